@@ -1,0 +1,181 @@
+/*
+ * pso_amd.h -- C-ABI of the MI355X-native PSO hot path (libpso_amd.so, gfx950).
+ *
+ * The reference (yaramohamadi/Pairwise_Sample_Optimization) is 100% Python; it has no FFI.  Every entry point below
+ * replaces an IMPLICIT kernel the reference runs through PyTorch/diffusers/peft on CUDA, and is bound from Python with
+ * ctypes by pairwise_sample_optimization_amd/_lib.py.  The `Replaces:` line of each function cites the reference call
+ * site (file:line) whose arithmetic it performs.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no framework types.  Every device buffer (weights, activations, workspace) is
+ *     owned by the caller; the library never allocates on the hot path.
+ *   - bf16 tensors are raw uint16 bit patterns; activations are channels-last (NHWC / [tokens][channels]).
+ *   - Every function returns 0 (PSO_OK) or an error code; pso_last_error() gives a thread-local message.
+ *   - Work is enqueued on the caller's hipStream_t (pass the stream handle as void*); nothing synchronises, so every
+ *     call is capturable into a hipGraph.
+ */
+#ifndef PSO_AMD_H
+#define PSO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSO_ABI_VERSION 1
+
+#define PSO_OK 0
+#define PSO_ERR_ARG 1
+#define PSO_ERR_HIP 2
+#define PSO_ERR_UNSUPPORTED 3
+
+/* dtype codes */
+#define PSO_F32 0
+#define PSO_BF16 1
+
+/* step modes */
+#define PSO_MODE_TURBO 0 /* Euler-ancestral (SDXL-Turbo)   DP/turbo_inference_with_logprob.py:24-116 */
+#define PSO_MODE_DMD 1   /* DDPM re-noise (SDXL-DMD2)      DP/distilled_inference_with_logprob.py:45-137 */
+
+/* Per-sample step coefficients, PSO_COEF_STRIDE floats each (host-computed in float32 from the scheduler tables):
+ *   TURBO: [sigma, sigma_up, dt = sigma_down - sigma, 2*sigma_up^2, log(sigma_up), log(sqrt(2*pi)), 0, 0]
+ *   DMD:   [sqrt(abar_t), sqrt(1-abar_t), sqrt(abar_prev), sqrt(1-abar_prev), 2*(1-abar_prev),
+ *           log(sqrt(1-abar_prev)), log(sqrt(2*pi)), 0]                                                        */
+#define PSO_COEF_STRIDE 8
+
+const char* pso_last_error(void);
+int pso_abi_version(void);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * PSO step log-prob (one scheduler step for a batch of B latents of n elements each).
+ * Replaces: turbo_step_with_logprob  DP/turbo_inference_with_logprob.py:24-116  (mode TURBO)
+ *           distilled_step_with_logprob DP/distilled_inference_with_logprob.py:45-137 (mode DMD)
+ * sample, prev_in, noise, prev_out are fp32 [B][n]; eps is [B][n] in eps_dtype.
+ * If prev_in is NULL the sampling branch runs: prev_out = mean + std * noise (noise [B][n], or [1][n] shared when
+ * noise_shared != 0 -- the DMD2 batch-shared draw, DP/distilled_inference_with_logprob.py:123-126).
+ * log_prob [B] fp32.  ws must hold pso_step_logprob_ws_bytes(B, n) bytes.
+ * ---------------------------------------------------------------------------------------------------------------- */
+size_t pso_step_logprob_ws_bytes(int B, int n);
+int pso_step_logprob(int mode, int B, int n, const float* sample, const void* eps, int eps_dtype,
+                     const float* prev_in, const float* noise, int noise_shared, const float* coef,
+                     float* prev_out, float* log_prob, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Fused PSO pairwise loss, forward and backward to the policy epsilon.
+ * Replaces: the 4 step log-probs + clipped log-ratio loss of one micro-step, T:810-850 / D:812-854 (forward), and
+ *           the autograd backward of that loss down to the UNet output (part of accelerator.backward, T:857).
+ * Layout: image i = 2*p + k (pair p, member k).  x, x_prev fp32 [2P][n]; eps_pol/eps_ref [2P][n] in eps_dtype;
+ * coef [2P][PSO_COEF_STRIDE]; pref [P][2] (+-1 or 0).
+ * fwd outputs: lp_out [2P][2] = (lp_theta, lp_ref) per image; loss_out [1] = mean over pairs; ws keeps the fp64
+ *   partial sums that bwd re-reads (keep it alive between the two calls).
+ * bwd output: deps_pol [2P][n] (deps_dtype) = (*grad_out or 1) * grad_scale * dL/d eps_pol; grad_out is a DEVICE
+ *   pointer to the upstream scalar gradient (may be NULL), so the call never synchronises.
+ * ---------------------------------------------------------------------------------------------------------------- */
+size_t pso_pair_loss_ws_bytes(int P, int n);
+int pso_pair_loss_fwd(int mode, int P, int n, const float* x, const float* x_prev, const void* eps_pol,
+                      const void* eps_ref, int eps_dtype, const float* coef, const float* pref, float beta,
+                      float clip_eps, float* lp_out, float* loss_out, void* ws, size_t ws_bytes, void* stream);
+int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_prev, const void* eps_pol,
+                      int eps_dtype, const float* coef, const float* pref, float beta, float clip_eps,
+                      const float* grad_out, float grad_scale, void* deps_pol, int deps_dtype, const void* ws,
+                      size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * bf16 MFMA GEMM, fp32 accumulate.
+ *   out[M][N] = alpha*(A1[M][K1].B1[N][K1]^T + A2[M][K2].B2[N][K2]^T) + bias[N] + rowbias[m/rows_per_group][N]
+ *               + resid[M][N]    (out bf16, f32, or f32 accumulate: out += ...)
+ * Replaces: every nn.Linear of the SDXL UNet/VAE (diffusers, run by cuBLAS) and the peft LoRA adapter
+ *           (peft 0.11.1 lora.Linear: base(x) + lora_B(lora_A(x)) * scaling), called from T:775-805, D:777-806,
+ *           DP/sdxl_turbo_with_logprob.py:126-132, DP/sdxl_dmd_with_logprob.py:117-122.  The (A2, B2) pair is the
+ *           LoRA up-projection fused as a K-tail; the same entry point computes the backward GEMMs (dX with W^T, dW).
+ * All A/B operands are bf16 with K contiguous; K1, K2 multiples of 8; rows 16-B aligned.
+ * ---------------------------------------------------------------------------------------------------------------- */
+int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
+             int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+             int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
+             void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).
+ * Input = channel concat of src1 [B][H][W][C1] and src2 [B][H][W][C2] (C2 may be 0); output [B][Ho][Wo][Cout] (ldo).
+ * Gather modes: PSO_CONV_NORMAL (stride/pad), PSO_CONV_UP2 (nearest 2x upsample fused, Ho=2H), PSO_CONV_T2
+ * (transposed stride-2: input-gradient of a stride-2 conv; weight = W^T per tap, unflipped).
+ * Epilogue as pso_gemm; rowbias is per image ([B][Cout], the ResnetBlock2D time-embedding add).
+ * Replaces: cuDNN conv2d of every diffusers ResnetBlock2D / Downsample2D / Upsample2D / conv_in / conv_out (UNet and
+ *           VAE decoder), plus the torch.cat of skip connections in the up blocks.
+ * ---------------------------------------------------------------------------------------------------------------- */
+#define PSO_CONV_NORMAL 1
+#define PSO_CONV_UP2 2
+#define PSO_CONV_T2 3
+int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+               int ks, int stride, int pad, const void* weight, int Cout, const void* a2, long lda2, int K2,
+               const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+               const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * GroupNorm (+ fused SiLU) on NHWC bf16, fp32 statistics.  stats [B][G][2] = (mean, rstd).
+ * Replaces: torch.nn.GroupNorm(32) + SiLU of diffusers ResnetBlock2D (norm1/norm2), Transformer2DModel.norm,
+ *           conv_norm_out (UNet, VAE decoder); its autograd backward (dx, optional dgamma/dbeta).
+ * ws: pso_group_norm_ws_bytes(B,HW,C) for fwd; + B*G*2 floats for bwd.  dadd (optional) is added to dx.
+ * ---------------------------------------------------------------------------------------------------------------- */
+size_t pso_group_norm_ws_bytes(int B, int HW, int C);
+int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, const void* gamma, const void* beta,
+                       int silu, void* y, float* stats, void* ws, size_t ws_bytes, void* stream);
+int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* dy, const float* stats,
+                       const void* gamma, const void* beta, int silu, const void* dadd, void* dx, float* dgamma,
+                       float* dbeta, int accumulate_dparams, void* ws, size_t ws_bytes, void* stream);
+
+/* LayerNorm over the last dim (C <= 2048), bf16 I/O, stats [M][2] fp32.
+ * Replaces: torch.nn.LayerNorm norm1/norm2/norm3 of diffusers BasicTransformerBlock (and its backward). */
+int pso_layer_norm_fwd(int M, int C, float eps, const void* x, long ldx, const void* gamma, const void* beta, void* y,
+                       long ldy, float* stats, void* stream);
+int pso_layer_norm_bwd(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                       const void* gamma, const void* dadd, long ldadd, void* dx, long lddx, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Flash attention, head dim 64, bf16 in/out (fp32 softmax).  Q [B][Sq][H*64] (row stride ldq, batch stride sq_b),
+ * K/V [B][Sk][H*64], O like Q; lse [B][H][Sq] (natural log of the scaled-score normaliser) for the backward.
+ * Replaces: F.scaled_dot_product_attention in diffusers AttnProcessor2_0 (attn1 self / attn2 cross attention of the
+ *           140 SDXL BasicTransformerBlocks) and its autograd backward.
+ * bwd: ws of pso_attention_bwd_ws_bytes(); for Sk <= 256 (cross-attention) dk/dv must be dense [B*Sk][.] with row
+ *      stride lddk/lddv and batch stride Sk*ld.
+ * ---------------------------------------------------------------------------------------------------------------- */
+int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
+                      long sk_b, const void* v, long ldv, long sv_b, float scale, void* o, long ldo, long so_b,
+                      float* lse, void* stream);
+size_t pso_attention_bwd_ws_bytes(int B, int H, int Sq, int Sk);
+int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
+                      long sk_b, const void* v, long ldv, long sv_b, const void* o, long ldo, long so_b,
+                      const float* lse, const void* dO, long lddo, long sdo_b, float scale, void* dq, long lddq,
+                      long sdq_b, void* dk, long lddk, long sdk_b, void* dv, long lddv, long sdv_b, void* ws,
+                      size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Element-wise / data movement (bf16 unless noted).
+ *   geglu: in [M][ldi] = [h | gate] (F each) -> out = h * gelu_erf(gate)     (diffusers GEGLU, FeedForward.net[0])
+ *   silu: y = x * sigmoid(x)                                                 (time-embedding nonlinearity)
+ *   timestep_embedding: t fp32 [n] -> out[:, out_col:out_col+dim] = [cos | sin](t * 10000^(-i/(dim/2)))
+ *                                                       (diffusers Timesteps, flip_sin_to_cos=True, shift=0)
+ *   transpose [R][C] -> [C][R]; im2col3 (3x3 pad 1, small C, zero padded to Kp columns); sumpool2 (2x2 sum, the
+ *   input-gradient of nearest-2x upsample); axpby y = a*x + b*z; casts; conv_weight_t ([Co][k][k][Ci] ->
+ *   [Ci][k][k][Co], flip=1 rotates the taps: the input-gradient weight of a stride-1 conv).
+ * ---------------------------------------------------------------------------------------------------------------- */
+int pso_geglu_fwd(long M, int F, const void* in, long ldi, void* out, long ldo, void* stream);
+int pso_geglu_bwd(long M, int F, const void* in, long ldi, const void* dout, long lddo, void* din, long lddi,
+                  void* stream);
+int pso_silu(long n, const void* x, void* y, void* stream);
+int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, int out_col, void* stream);
+int pso_transpose(int R, int C, const void* in, long ldi, void* out, long ldo, void* stream);
+int pso_im2col3(int B, int H, int W, int C, const void* in, void* out, int Kp, void* stream);
+int pso_sumpool2(int B, int H, int W, int C, const void* in, const void* dadd, void* out, void* stream);
+int pso_axpby(long n, float a, const void* x, float b, const void* z, void* y, void* stream);
+int pso_cast_f32_bf16(long n, const float* x, float scale, void* y, void* stream);
+int pso_cast_bf16_f32(long n, const void* x, float* y, void* stream);
+int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSO_AMD_H */

@@ -1,0 +1,115 @@
+"""ctypes binding of libpso_amd.so (the C-ABI declared in include/pso_amd.h).
+
+The library is built in-tree by `make -C pairwise_sample_optimization_amd/csrc` (see __graft_entry__.build()).
+There is NO fallback: if the shared object is missing or fails to load, every op raises.  torch is imported first so
+that the HIP runtime torch ships (SONAME libamdhip64.so.7) is the one the library binds to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before ours)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpso_amd.so")
+
+PSO_F32 = 0
+PSO_BF16 = 1
+MODE_TURBO = 0
+MODE_DMD = 1
+COEF_STRIDE = 8
+
+_lib = None
+
+vp = ctypes.c_void_p
+ci = ctypes.c_int
+cf = ctypes.c_float
+csz = ctypes.c_size_t
+ci64 = ctypes.c_int64
+cl = ctypes.c_long
+
+# name -> (restype, argtypes).  Kept in sync with include/pso_amd.h (tests/test_abi.py checks every symbol).
+SIGNATURES = {
+    "pso_last_error": (ctypes.c_char_p, []),
+    "pso_abi_version": (ci, []),
+    "pso_step_logprob_ws_bytes": (csz, [ci, ci]),
+    "pso_step_logprob": (ci, [ci, ci, ci, vp, vp, ci, vp, vp, ci, vp, vp, vp, vp, csz, vp]),
+    "pso_pair_loss_ws_bytes": (csz, [ci, ci]),
+    "pso_pair_loss_fwd": (ci, [ci, ci, ci, vp, vp, vp, vp, ci, vp, vp, cf, cf, vp, vp, vp, csz, vp]),
+    "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
+    "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
+                      vp]),
+    "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
+                        cl, vp, cl, vp, cl, ci, ci, vp]),
+    "pso_group_norm_ws_bytes": (csz, [ci, ci, ci]),
+    "pso_group_norm_fwd": (ci, [ci, ci, ci, ci, cf, vp, vp, vp, ci, vp, vp, vp, csz, vp]),
+    "pso_group_norm_bwd": (ci, [ci, ci, ci, ci, vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, ci, vp, csz, vp]),
+    "pso_layer_norm_fwd": (ci, [ci, ci, cf, vp, cl, vp, vp, vp, cl, vp, vp]),
+    "pso_layer_norm_bwd": (ci, [ci, ci, vp, cl, vp, cl, vp, vp, vp, cl, vp, cl, vp]),
+    "pso_attention_fwd": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, vp, vp]),
+    "pso_attention_bwd_ws_bytes": (csz, [ci, ci, ci, ci]),
+    "pso_attention_bwd": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, vp, cl, cl, vp, cl, cl, vp, vp, cl, cl, cf,
+                               vp, cl, cl, vp, cl, cl, vp, cl, cl, vp, csz, vp]),
+    "pso_geglu_fwd": (ci, [cl, ci, vp, cl, vp, cl, vp]),
+    "pso_geglu_bwd": (ci, [cl, ci, vp, cl, vp, cl, vp, cl, vp]),
+    "pso_silu": (ci, [cl, vp, vp, vp]),
+    "pso_timestep_embedding": (ci, [ci, ci, vp, vp, cl, ci, vp]),
+    "pso_transpose": (ci, [ci, ci, vp, cl, vp, cl, vp]),
+    "pso_im2col3": (ci, [ci, ci, ci, ci, vp, vp, ci, vp]),
+    "pso_sumpool2": (ci, [ci, ci, ci, ci, vp, vp, vp, vp]),
+    "pso_axpby": (ci, [cl, cf, vp, cf, vp, vp, vp]),
+    "pso_cast_f32_bf16": (ci, [cl, vp, cf, vp, vp]),
+    "pso_cast_bf16_f32": (ci, [cl, vp, vp, vp]),
+    "pso_conv_weight_t": (ci, [ci, ci, ci, ci, vp, vp, vp]),
+}
+
+
+class PsoLibError(RuntimeError):
+    pass
+
+
+def _bind(lib):
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load (once) and return the bound library; raises if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PsoLibError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                              "(no CPU fallback exists)")
+        l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _bind(l)
+        _lib = l
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().pso_last_error().decode(errors="replace")
+        raise PsoLibError(f"{what} failed (rc={rc}): {msg}")
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return PSO_F32
+    if t.dtype == torch.bfloat16:
+        return PSO_BF16
+    raise PsoLibError(f"unsupported dtype {t.dtype}")
+
+
+def require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise PsoLibError("libpso_amd ops take device tensors only (no CPU fallback)")

@@ -1,0 +1,280 @@
+// Element-wise and data-movement kernels of the UNet / VAE hot path (bf16, 16-B vector access).
+//
+//   GEGLU fwd/bwd         diffusers GEGLU (FeedForward.net[0]): h, gate = proj(x).chunk(2); h * gelu(gate) (erf gelu)
+//   SiLU                  nonlinearity applied to the time embedding before every time_emb_proj (ResnetBlock2D)
+//   timestep embedding    diffusers Timesteps(flip_sin_to_cos=True, downscale_freq_shift=0) for time_proj and
+//                         add_time_proj (UNet2DConditionModel.forward, SDXL "text_time" added condition)
+//   transpose             [R][C] -> [C][R] bf16 (operands of the reduction-over-tokens GEMMs in backward)
+//   im2col (small C)      conv_in (C=4) and the input-gradient of conv_out (C=4) as plain GEMMs
+//   sum-pool 2x2          input-gradient of the nearest-2x upsample of Upsample2D
+//   add / scale / cast    gradient merges, fp32 -> bf16 casts
+#include "common.h"
+
+__device__ __forceinline__ void unpack8e(uint4 v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bf2f(w[i] & 0xffff);
+    f[2 * i + 1] = bf2f(w[i] >> 16);
+  }
+}
+__device__ __forceinline__ uint4 pack8e(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+
+static int grid_for(long n, int per_thread = 1) {
+  long g = (n / per_thread + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (int)(g < 1 ? 1 : g);
+}
+
+#define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+
+__device__ __forceinline__ float gelu_erf(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float g) {
+  const float cdf = 0.5f * (1.f + erff(g * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * g * g);
+  return cdf + g * pdf;
+}
+
+// in [M][ld_in] holding [h | gate] (F each); out [M][F] = h * gelu(gate)
+__global__ void geglu_fwd_kernel(long M, int F, const bf16_t* __restrict__ in, long ldi, bf16_t* __restrict__ out,
+                                 long ldo) {
+  const int F8 = F / 8;
+  GRID_STRIDE(v, M * F8) {
+    const long m = v / F8;
+    const int c = (int)(v - m * F8) * 8;
+    float h[8], g[8], o[8];
+    unpack8e(*reinterpret_cast<const uint4*>(in + m * ldi + c), h);
+    unpack8e(*reinterpret_cast<const uint4*>(in + m * ldi + F + c), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = h[j] * gelu_erf(g[j]);
+    *reinterpret_cast<uint4*>(out + m * ldo + c) = pack8e(o);
+  }
+}
+
+// dout [M][F] -> din [M][2F] = [dout*gelu(g) | dout*h*gelu'(g)]
+__global__ void geglu_bwd_kernel(long M, int F, const bf16_t* __restrict__ in, long ldi,
+                                 const bf16_t* __restrict__ dout, long lddo, bf16_t* __restrict__ din, long lddi) {
+  const int F8 = F / 8;
+  GRID_STRIDE(v, M * F8) {
+    const long m = v / F8;
+    const int c = (int)(v - m * F8) * 8;
+    float h[8], g[8], d[8], dh[8], dg[8];
+    unpack8e(*reinterpret_cast<const uint4*>(in + m * ldi + c), h);
+    unpack8e(*reinterpret_cast<const uint4*>(in + m * ldi + F + c), g);
+    unpack8e(*reinterpret_cast<const uint4*>(dout + m * lddo + c), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dh[j] = d[j] * gelu_erf(g[j]);
+      dg[j] = d[j] * h[j] * gelu_erf_grad(g[j]);
+    }
+    *reinterpret_cast<uint4*>(din + m * lddi + c) = pack8e(dh);
+    *reinterpret_cast<uint4*>(din + m * lddi + F + c) = pack8e(dg);
+  }
+}
+
+__global__ void silu_kernel(long n8, const bf16_t* __restrict__ x, bf16_t* __restrict__ y) {
+  GRID_STRIDE(v, n8) {
+    float a[8];
+    unpack8e(*reinterpret_cast<const uint4*>(x + v * 8), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = a[j] / (1.f + __expf(-a[j]));
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8e(a);
+  }
+}
+
+// t [n] (fp32) -> out [n][dim] (bf16 at column offset out_col, row stride ldo): [cos(t*f) | sin(t*f)],
+// f_i = exp(-ln(10000) * i / half)   (flip_sin_to_cos=True, downscale_freq_shift=0, scale=1)
+__global__ void timestep_embed_kernel(int n, int dim, const float* __restrict__ t, bf16_t* __restrict__ out, long ldo,
+                                      int out_col) {
+  const int half = dim / 2;
+  GRID_STRIDE(i, (long)n * half) {
+    const int r = (int)(i / half), k = (int)(i - (long)r * half);
+    const float expo = -9.210340371976184f * (float)k / (float)half;  // -ln(10000)*k/half
+    const float arg = t[r] * expf(expo);
+    out[(long)r * ldo + out_col + k] = f2bf(cosf(arg));
+    out[(long)r * ldo + out_col + half + k] = f2bf(sinf(arg));
+  }
+}
+
+// 32x32 tiled transpose, bf16: in [R][C] (ldi) -> out [C][R] (ldo)
+__global__ void transpose_kernel(int R, int C, const bf16_t* __restrict__ in, long ldi, bf16_t* __restrict__ out,
+                                 long ldo) {
+  __shared__ bf16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? in[(long)r * ldi + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[(long)c * ldo + r] = tile[tx][i];
+  }
+}
+
+// NHWC small-channel im2col for 3x3/pad 1/stride 1: in [B][H][W][C] -> out [B*H*W][Kp] (Kp >= 9C, zero padded),
+// column order (kh, kw, c) to match [Cout][kh][kw][C] weights.
+__global__ void im2col3_kernel(int B, int H, int W, int C, const bf16_t* __restrict__ in, int flip,
+                               bf16_t* __restrict__ out, int Kp) {
+  GRID_STRIDE(i, (long)B * H * W * Kp) {
+    const long pix = i / Kp;
+    const int k = (int)(i - pix * Kp);
+    bf16_t v = 0;
+    if (k < 9 * C) {
+      const int tap = k / C, c = k - tap * C;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int b = (int)(pix / ((long)H * W));
+      const int rem = (int)(pix - (long)b * H * W);
+      const int y = rem / W, x = rem - y * W;
+      const int iy = y + kh - 1, ix = x + kw - 1;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = in[(((long)b * H + iy) * W + ix) * C + c];
+    }
+    out[i] = v;
+  }
+}
+
+// upsample-2x input gradient: in [B][2H][2W][C] -> out [B][H][W][C] = sum of the 2x2 block (+ dadd)
+__global__ void sumpool2_kernel(int B, int H, int W, int C, const bf16_t* __restrict__ in,
+                                const bf16_t* __restrict__ dadd, bf16_t* __restrict__ out) {
+  const int C8 = C / 8;
+  GRID_STRIDE(v, (long)B * H * W * C8) {
+    const long pix = v / C8;
+    const int c = (int)(v - pix * C8) * 8;
+    const int b = (int)(pix / ((long)H * W));
+    const int rem = (int)(pix - (long)b * H * W);
+    const int y = rem / W, x = rem - y * W;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float a[8];
+        unpack8e(*reinterpret_cast<const uint4*>(in + (((long)b * 2 * H + 2 * y + dy) * 2 * W + 2 * x + dx) * C + c), a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += a[j];
+      }
+    if (dadd) {
+      float a[8];
+      unpack8e(*reinterpret_cast<const uint4*>(dadd + pix * C + c), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += a[j];
+    }
+    *reinterpret_cast<uint4*>(out + pix * C + c) = pack8e(acc);
+  }
+}
+
+// y = a*x + b*z (bf16 in, bf16 out); z may be null
+__global__ void axpby_kernel(long n8, float a, const bf16_t* __restrict__ x, float b, const bf16_t* __restrict__ z,
+                             bf16_t* __restrict__ y) {
+  GRID_STRIDE(v, n8) {
+    float p[8], q[8];
+    unpack8e(*reinterpret_cast<const uint4*>(x + v * 8), p);
+    if (z) unpack8e(*reinterpret_cast<const uint4*>(z + v * 8), q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = a * p[j] + (z ? b * q[j] : 0.f);
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8e(p);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(long n, const float* __restrict__ x, float scale, bf16_t* __restrict__ y) {
+  GRID_STRIDE(i, n) y[i] = f2bf(x[i] * scale);
+}
+__global__ void cast_bf16_f32_kernel(long n, const bf16_t* __restrict__ x, float* __restrict__ y) {
+  GRID_STRIDE(i, n) y[i] = bf2f(x[i]);
+}
+
+// conv weight [Co][kh][kw][Ci] -> input-gradient weight [Ci][kh'][kw'][Co]; flip=1: kh'=ks-1-kh (stride-1 bwd)
+__global__ void conv_weight_t_kernel(int Co, int ks, int Ci, int flip, const bf16_t* __restrict__ w,
+                                     bf16_t* __restrict__ wt) {
+  GRID_STRIDE(i, (long)Co * ks * ks * Ci) {
+    const int ci = (int)(i % Ci);
+    long r = i / Ci;
+    const int kw = (int)(r % ks);
+    r /= ks;
+    const int kh = (int)(r % ks);
+    const int co = (int)(r / ks);
+    const int kh2 = flip ? ks - 1 - kh : kh, kw2 = flip ? ks - 1 - kw : kw;
+    wt[(((long)ci * ks + kh2) * ks + kw2) * Co + co] = w[i];
+  }
+}
+
+extern "C" {
+
+int pso_geglu_fwd(long M, int F, const void* in, long ldi, void* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(F % 8 == 0 && ldi % 8 == 0 && ldo % 8 == 0 && in && out, "pso_geglu_fwd: bad args");
+  geglu_fwd_kernel<<<grid_for(M * (F / 8)), 256, 0, (hipStream_t)stream>>>(M, F, (const bf16_t*)in, ldi,
+                                                                          (bf16_t*)out, ldo);
+  return pso_check_launch("pso_geglu_fwd");
+}
+
+int pso_geglu_bwd(long M, int F, const void* in, long ldi, const void* dout, long lddo, void* din, long lddi,
+                  void* stream) {
+  PSO_ARG_CHECK(F % 8 == 0 && ldi % 8 == 0 && lddo % 8 == 0 && lddi % 8 == 0 && in && dout && din,
+                "pso_geglu_bwd: bad args");
+  geglu_bwd_kernel<<<grid_for(M * (F / 8)), 256, 0, (hipStream_t)stream>>>(M, F, (const bf16_t*)in, ldi,
+                                                                          (const bf16_t*)dout, lddo, (bf16_t*)din,
+                                                                          lddi);
+  return pso_check_launch("pso_geglu_bwd");
+}
+
+int pso_silu(long n, const void* x, void* y, void* stream) {
+  PSO_ARG_CHECK(n % 8 == 0 && x && y, "pso_silu: n must be a multiple of 8");
+  silu_kernel<<<grid_for(n / 8), 256, 0, (hipStream_t)stream>>>(n / 8, (const bf16_t*)x, (bf16_t*)y);
+  return pso_check_launch("pso_silu");
+}
+
+int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, int out_col, void* stream) {
+  PSO_ARG_CHECK(dim % 2 == 0 && t && out, "pso_timestep_embedding: bad args");
+  timestep_embed_kernel<<<grid_for((long)n * dim / 2), 256, 0, (hipStream_t)stream>>>(n, dim, t, (bf16_t*)out, ldo,
+                                                                                      out_col);
+  return pso_check_launch("pso_timestep_embedding");
+}
+
+int pso_transpose(int R, int C, const void* in, long ldi, void* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(in && out, "pso_transpose: null");
+  dim3 grid(cdiv(C, 64), cdiv(R, 64));
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(R, C, (const bf16_t*)in, ldi, (bf16_t*)out, ldo);
+  return pso_check_launch("pso_transpose");
+}
+
+int pso_im2col3(int B, int H, int W, int C, const void* in, void* out, int Kp, void* stream) {
+  PSO_ARG_CHECK(Kp >= 9 * C && in && out, "pso_im2col3: Kp < 9C");
+  im2col3_kernel<<<grid_for((long)B * H * W * Kp), 256, 0, (hipStream_t)stream>>>(B, H, W, C, (const bf16_t*)in, 0,
+                                                                                  (bf16_t*)out, Kp);
+  return pso_check_launch("pso_im2col3");
+}
+
+int pso_sumpool2(int B, int H, int W, int C, const void* in, const void* dadd, void* out, void* stream) {
+  PSO_ARG_CHECK(C % 8 == 0 && in && out, "pso_sumpool2: C %% 8");
+  sumpool2_kernel<<<grid_for((long)B * H * W * C / 8), 256, 0, (hipStream_t)stream>>>(
+      B, H, W, C, (const bf16_t*)in, (const bf16_t*)dadd, (bf16_t*)out);
+  return pso_check_launch("pso_sumpool2");
+}
+
+int pso_axpby(long n, float a, const void* x, float b, const void* z, void* y, void* stream) {
+  PSO_ARG_CHECK(n % 8 == 0 && x && y, "pso_axpby: n %% 8");
+  axpby_kernel<<<grid_for(n / 8), 256, 0, (hipStream_t)stream>>>(n / 8, a, (const bf16_t*)x, b, (const bf16_t*)z,
+                                                                 (bf16_t*)y);
+  return pso_check_launch("pso_axpby");
+}
+
+int pso_cast_f32_bf16(long n, const float* x, float scale, void* y, void* stream) {
+  cast_f32_bf16_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(n, x, scale, (bf16_t*)y);
+  return pso_check_launch("pso_cast_f32_bf16");
+}
+
+int pso_cast_bf16_f32(long n, const void* x, float* y, void* stream) {
+  cast_bf16_f32_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(n, (const bf16_t*)x, y);
+  return pso_check_launch("pso_cast_bf16_f32");
+}
+
+int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt, void* stream) {
+  conv_weight_t_kernel<<<grid_for((long)Co * ks * ks * Ci), 256, 0, (hipStream_t)stream>>>(
+      Co, ks, Ci, flip, (const bf16_t*)w, (bf16_t*)wt);
+  return pso_check_launch("pso_conv_weight_t");
+}
+
+}  // extern "C"

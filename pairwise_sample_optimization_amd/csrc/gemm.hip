@@ -1,0 +1,344 @@
+// bf16 MFMA GEMM / implicit-GEMM convolution for gfx950 (CDNA4), fp32 accumulate.
+//
+//   out[M][N] = epilogue( alpha * ( A1[M][K1] . B1[N][K1]^T  +  A2[M][K2] . B2[N][K2]^T ) )
+//   epilogue  = + bias[N] + rowbias[m / rows_per_group][N] + resid[M][N]   -> bf16 | f32 | f32 accumulate
+//
+// Replaces the implicit cuBLAS GEMMs (every nn.Linear of the SDXL UNet / VAE and the peft LoRA product, SURVEY §2
+// "cuBLAS GEMM") and the cuDNN conv2d (SURVEY §2 "cuDNN conv2d"): the conv is an implicit GEMM whose A operand is
+// gathered on the fly from an NHWC image (M = B*Ho*Wo pixels, K = kh*kw*Cin), with three gather modes:
+//   NORMAL  iy = oy*S + kh - P        (conv 3x3/1x1, stride 1 or 2)
+//   UP2     iy = (oy + kh - P) >> 1   (nearest 2x upsample fused into the following conv, diffusers Upsample2D)
+//   T2      iy = (oy + P - kh) / 2    (transposed stride-2 conv: input-gradient of the Downsample2D conv)
+// and an optional second channel source (torch.cat([h, skip], dim=1) of the up blocks, fused into the gather).
+// The second (A2, B2) operand pair is the LoRA up-projection fused as a K-tail: y = x W^T + (x A^T)(s B)^T.
+//
+// Tiling: 256 threads = 4 waves (2 x 2), block tile BM x BN x 64, wave tile (BM/2) x (BN/2) built from
+// v_mfma_f32_16x16x32_bf16.  Operands are staged global -> VGPR -> LDS (double buffered, one barrier per K-tile) with
+// an XOR swizzle (chunk ^ (row & 7)) that makes both the ds_write_b128 and the ds_read_b128 fragment reads
+// conflict-free on 128-B rows.  The MFMA is issued with the B (weight) fragment first so that every lane ends up
+// holding 4 consecutive output columns of one row -> 8-B / 16-B vector epilogue stores.
+#include "common.h"
+
+#define GEMM_THREADS 256
+#define BK 64
+
+struct ConvGeom {
+  int mode;      // 0 = dense A, else PSO_CONV_* gather
+  const bf16_t* src2;  // second channel source (concat) or null
+  int C1, C2;    // channels of src1 (A1) and src2
+  int H, W;      // input spatial size (source grid)
+  int Ho, Wo;    // output spatial size
+  int ks, stride, pad;
+};
+
+struct GemmArgs {
+  const bf16_t* a1; long lda1; int K1;
+  const bf16_t* b1; long ldb1;
+  const bf16_t* a2; long lda2; int K2;
+  const bf16_t* b2; long ldb2;
+  int M, N;
+  ConvGeom conv;
+  float alpha;
+  const bf16_t* bias;
+  const bf16_t* rowbias; long ld_rowbias; int rows_per_group;
+  const bf16_t* resid; long ldr;
+  void* out; long ldo; int out_dtype; int accumulate;
+  int vec_ok;  // 4-wide epilogue vectors are aligned
+};
+
+__device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ (r & 7)) << 3); }
+
+template <int BM, int BN>
+struct Tile {
+  static constexpr int A_CH = BM * BK / 8 / GEMM_THREADS;  // 16-B chunks per thread
+  static constexpr int B_CH = BN * BK / 8 / GEMM_THREADS;
+};
+
+// ---- per-row conv coordinates (precomputed once per thread) ----
+struct RowCoord {
+  int b, oy, ox;
+  bool valid;
+};
+
+__device__ __forceinline__ uint4 load_chunk_dense(const bf16_t* p, long ld, int row, int nrows, int k, int K) {
+  if (row < nrows && k < K) return *reinterpret_cast<const uint4*>(p + (long)row * ld + k);
+  return make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint4 load_chunk_conv(const GemmArgs& g, const RowCoord& rc, int k) {
+  const ConvGeom& cv = g.conv;
+  const int Ct = cv.C1 + cv.C2;
+  if (!rc.valid || k >= g.K1) return make_uint4(0, 0, 0, 0);
+  const int tap = k / Ct;
+  const int c = k - tap * Ct;
+  const int kh = tap / cv.ks, kw = tap - kh * cv.ks;
+  int iy, ix;
+  if (cv.mode == PSO_CONV_NORMAL) {
+    iy = rc.oy * cv.stride + kh - cv.pad;
+    ix = rc.ox * cv.stride + kw - cv.pad;
+    if (iy < 0 || iy >= cv.H || ix < 0 || ix >= cv.W) return make_uint4(0, 0, 0, 0);
+  } else if (cv.mode == PSO_CONV_UP2) {
+    const int uy = rc.oy + kh - cv.pad, ux = rc.ox + kw - cv.pad;
+    if (uy < 0 || uy >= 2 * cv.H || ux < 0 || ux >= 2 * cv.W) return make_uint4(0, 0, 0, 0);
+    iy = uy >> 1;
+    ix = ux >> 1;
+  } else {  // T2
+    const int ty = rc.oy + cv.pad - kh, tx = rc.ox + cv.pad - kw;
+    if (ty < 0 || tx < 0 || (ty & 1) || (tx & 1)) return make_uint4(0, 0, 0, 0);
+    iy = ty >> 1;
+    ix = tx >> 1;
+    if (iy >= cv.H || ix >= cv.W) return make_uint4(0, 0, 0, 0);
+  }
+  const long pix = ((long)rc.b * cv.H + iy) * cv.W + ix;
+  if (c < cv.C1) return *reinterpret_cast<const uint4*>(g.a1 + pix * cv.C1 + c);
+  return *reinterpret_cast<const uint4*>(cv.src2 + pix * cv.C2 + (c - cv.C1));
+}
+
+template <int BM, int BN, bool CONV>
+__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) {
+  using T = Tile<BM, BN>;
+  constexpr int MI = BM / 32;  // 16-row subtiles per wave
+  constexpr int NJ = BN / 32;  // 16-col subtiles per wave
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM + BN) * BK];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware block order: blocks b, b+8, b+16 ... share an XCD; give each XCD a contiguous run of tiles.
+  const int nbn = (g.N + BN - 1) / BN, nbm = (g.M + BM - 1) / BM;
+  const int nblk = nbn * nbm;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    if (nblk >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const int nt1 = (g.K1 + BK - 1) / BK;
+  const int nt2 = g.a2 ? (g.K2 + BK - 1) / BK : 0;
+  const int nt = nt1 + nt2;
+
+  // staging coordinates: chunk q = tid + 256*i -> row q/8, k-chunk q%8
+  RowCoord rc[T::A_CH];
+  if (CONV) {
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      const int m = m0 + (tid + GEMM_THREADS * i) / 8;
+      const int hw = g.conv.Ho * g.conv.Wo;
+      rc[i].valid = m < g.M;
+      const int mm = rc[i].valid ? m : 0;
+      rc[i].b = mm / hw;
+      const int rem = mm - rc[i].b * hw;
+      rc[i].oy = rem / g.conv.Wo;
+      rc[i].ox = rem - rc[i].oy * g.conv.Wo;
+    }
+  }
+  uint4 ra[T::A_CH], rb[T::B_CH];
+
+  auto load_tile = [&](int t) {
+    const bool second = t >= nt1;
+    const int k0 = (second ? t - nt1 : t) * BK;
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      const int q = tid + GEMM_THREADS * i;
+      const int row = q >> 3, kc = (q & 7) * 8;
+      if (second) ra[i] = load_chunk_dense(g.a2, g.lda2, m0 + row, g.M, k0 + kc, g.K2);
+      else if (CONV) ra[i] = load_chunk_conv(g, rc[i], k0 + kc);
+      else ra[i] = load_chunk_dense(g.a1, g.lda1, m0 + row, g.M, k0 + kc, g.K1);
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i) {
+      const int q = tid + GEMM_THREADS * i;
+      const int row = q >> 3, kc = (q & 7) * 8;
+      rb[i] = second ? load_chunk_dense(g.b2, g.ldb2, n0 + row, g.N, k0 + kc, g.K2)
+                     : load_chunk_dense(g.b1, g.ldb1, n0 + row, g.N, k0 + kc, g.K1);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16_t* la = lds[buf];
+    bf16_t* lb = lds[buf] + BM * BK;
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      const int q = tid + GEMM_THREADS * i;
+      *reinterpret_cast<uint4*>(la + swz(q >> 3, q & 7)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i) {
+      const int q = tid + GEMM_THREADS * i;
+      *reinterpret_cast<uint4*>(lb + swz(q >> 3, q & 7)) = rb[i];
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load_tile(t + 1);
+    const bf16_t* la = lds[cur];
+    const bf16_t* lb = lds[cur] + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / 2) + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / 2) + j * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds out[m][n0..n0+3] for each (i, j) ----
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * (BM / 2) + i * 16 + fr;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + fk * 4;
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
+                    acc[i][j][3] * g.alpha};
+      const bool full = g.vec_ok && (n + 4 <= g.N);
+      if (full) {
+        if (g.bias) {
+          const uint2 bv = *reinterpret_cast<const uint2*>(g.bias + n);
+          v[0] += bf2f(bv.x & 0xffff); v[1] += bf2f(bv.x >> 16); v[2] += bf2f(bv.y & 0xffff); v[3] += bf2f(bv.y >> 16);
+        }
+        if (g.rowbias) {
+          const uint2 bv = *reinterpret_cast<const uint2*>(g.rowbias + (long)(m / g.rows_per_group) * g.ld_rowbias + n);
+          v[0] += bf2f(bv.x & 0xffff); v[1] += bf2f(bv.x >> 16); v[2] += bf2f(bv.y & 0xffff); v[3] += bf2f(bv.y >> 16);
+        }
+        if (g.resid) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(g.resid + (long)m * g.ldr + n);
+          v[0] += bf2f(rv.x & 0xffff); v[1] += bf2f(rv.x >> 16); v[2] += bf2f(rv.y & 0xffff); v[3] += bf2f(rv.y >> 16);
+        }
+        if (g.out_dtype == PSO_BF16) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n) =
+              make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        } else {
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n);
+          if (g.accumulate) {
+            const float4 old = *o;
+            v[0] += old.x; v[1] += old.y; v[2] += old.z; v[3] += old.w;
+          }
+          *o = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      } else {
+        for (int r = 0; r < 4 && n + r < g.N; ++r) {
+          float x = v[r];
+          if (g.bias) x += bf2f(g.bias[n + r]);
+          if (g.rowbias) x += bf2f(g.rowbias[(long)(m / g.rows_per_group) * g.ld_rowbias + n + r]);
+          if (g.resid) x += bf2f(g.resid[(long)m * g.ldr + n + r]);
+          if (g.out_dtype == PSO_BF16) {
+            reinterpret_cast<bf16_t*>(g.out)[(long)m * g.ldo + n + r] = f2bf(x);
+          } else {
+            float* o = reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n + r;
+            *o = g.accumulate ? *o + x : x;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+static int launch(const GemmArgs& g, hipStream_t st) {
+  const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  if (g.conv.mode) gemm_bf16_kernel<BM, BN, true><<<nblk, GEMM_THREADS, 0, st>>>(g);
+  else gemm_bf16_kernel<BM, BN, false><<<nblk, GEMM_THREADS, 0, st>>>(g);
+  return pso_check_launch("pso_gemm");
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
+
+static int run_gemm(GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return PSO_OK;
+  g.vec_ok = (g.ldo % 4) == 0 && (g.out_dtype == PSO_F32 ? al16(g.out) : al8(g.out)) &&
+             (!g.resid || ((g.ldr % 4) == 0 && al8(g.resid))) && (!g.bias || al8(g.bias)) &&
+             (!g.rowbias || (al8(g.rowbias) && (g.ld_rowbias % 4) == 0));
+  // Small-N / small-M shapes: 64-wide tiles waste less.
+  if (g.N <= 64) return launch<128, 64>(g, st);
+  if (g.M <= 64) return launch<64, 128>(g, st);
+  return launch<128, 128>(g, st);
+}
+
+extern "C" {
+
+int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
+             int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+             int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
+             void* stream) {
+  PSO_ARG_CHECK(M >= 0 && N >= 0 && K1 >= 0 && (K1 % 8) == 0, "pso_gemm: need K1 %% 8 == 0 (K1=%d)", K1);
+  PSO_ARG_CHECK(a1 && b1 && out, "pso_gemm: null operand");
+  PSO_ARG_CHECK(al16(a1) && al16(b1) && (lda1 % 8) == 0 && (ldb1 % 8) == 0, "pso_gemm: A1/B1 must be 16-B aligned rows");
+  PSO_ARG_CHECK(!a2 || (b2 && (K2 % 8) == 0 && al16(a2) && al16(b2) && (lda2 % 8) == 0 && (ldb2 % 8) == 0),
+                "pso_gemm: bad second operand");
+  PSO_ARG_CHECK(out_dtype == PSO_BF16 || out_dtype == PSO_F32, "pso_gemm: bad out dtype");
+  PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_gemm: accumulate needs f32 output");
+  PSO_ARG_CHECK(!rowbias || rows_per_group > 0, "pso_gemm: rowbias needs rows_per_group > 0");
+  GemmArgs g{};
+  g.a1 = (const bf16_t*)a1; g.lda1 = lda1; g.K1 = K1;
+  g.b1 = (const bf16_t*)b1; g.ldb1 = ldb1;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
+  g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
+  g.M = M; g.N = N;
+  g.alpha = alpha;
+  g.bias = (const bf16_t*)bias;
+  g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
+  g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  return run_gemm(g, (hipStream_t)stream);
+}
+
+int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+               int ks, int stride, int pad, const void* weight, int Cout, const void* a2, long lda2, int K2,
+               const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+               const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate, void* stream) {
+  PSO_ARG_CHECK(mode == PSO_CONV_NORMAL || mode == PSO_CONV_UP2 || mode == PSO_CONV_T2, "pso_conv2d: bad mode");
+  PSO_ARG_CHECK(src1 && weight && out, "pso_conv2d: null operand");
+  PSO_ARG_CHECK((C1 % 64) == 0 && (C2 % 64) == 0 && (C2 == 0 || src2),
+                "pso_conv2d: channel sources must be multiples of 64 (C1=%d C2=%d); use im2col for small C", C1, C2);
+  PSO_ARG_CHECK(al16(src1) && (!src2 || al16(src2)) && al16(weight), "pso_conv2d: alignment");
+  PSO_ARG_CHECK(ks == 1 || ks == 3, "pso_conv2d: ks must be 1 or 3");
+  PSO_ARG_CHECK(mode != PSO_CONV_UP2 || (Ho == 2 * H && Wo == 2 * W && stride == 1), "pso_conv2d: UP2 geometry");
+  PSO_ARG_CHECK(!a2 || ((K2 % 8) == 0 && b2 && al16(a2) && al16(b2)), "pso_conv2d: bad second operand");
+  PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_conv2d: accumulate needs f32 output");
+  GemmArgs g{};
+  const int Ct = C1 + C2;
+  g.a1 = (const bf16_t*)src1; g.lda1 = 0; g.K1 = ks * ks * Ct;
+  g.b1 = (const bf16_t*)weight; g.ldb1 = g.K1;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
+  g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
+  g.M = B * Ho * Wo; g.N = Cout;
+  g.conv.mode = mode; g.conv.src2 = (const bf16_t*)src2; g.conv.C1 = C1; g.conv.C2 = C2;
+  g.conv.H = H; g.conv.W = W; g.conv.Ho = Ho; g.conv.Wo = Wo; g.conv.ks = ks; g.conv.stride = stride; g.conv.pad = pad;
+  g.alpha = alpha;
+  g.bias = (const bf16_t*)bias;
+  g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = Ho * Wo;
+  g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  return run_gemm(g, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,429 @@
+// GroupNorm(+SiLU) and LayerNorm, forward and backward, on channels-last bf16 activations (fp32 statistics).
+//
+// Replaces the implicit norm kernels of the diffusers SDXL UNet/VAE (SURVEY §2 "GroupNorm(32) + SiLU", "LayerNorm"):
+//   ResnetBlock2D.norm1/norm2 + SiLU, Transformer2DModel.norm (eps 1e-6), conv_norm_out + SiLU, VAE GroupNorms,
+//   BasicTransformerBlock.norm1/2/3 (LayerNorm eps 1e-5).
+//
+// GroupNorm on NHWC: a group is Cg = C/G channels of every pixel of one image.  Each pass streams whole pixel rows
+// (C contiguous channels -> 16-B coalesced loads; a group-major walk would read 20-B fragments at C=320):
+//   partial  : block = (pixel chunk, image); thread (slot, 8-channel chunk) accumulates per-channel sums
+//              fwd: (sum x, sum x^2)      bwd: (sum dz, sum dz*xhat)   -> ws [B][chunks][C][2] (fp32)
+//   finalize : one thread per (image, group), fixed-order fp64 combine -> (mean, rstd) | (mean dxhat, mean dxhat*xhat)
+//   apply    : element-wise, 8 channels per thread: y = silu?((x-mean)*rstd*gamma + beta)
+//              dx = rstd*(dz*gamma - a - xhat*b) (+ residual gradient), dz = dy*silu'(z) when SiLU is fused.
+// Backward also emits per-channel dgamma/dbeta partial sums (full-UNet gradients, config 3) when asked.
+#include "common.h"
+
+#define GN_ROWS 64  // pixels per partial block
+
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bf2f(w[i] & 0xffff);
+    f[2 * i + 1] = bf2f(w[i] >> 16);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// ---------------------------------------------------------------------------------------------------------------
+// partial sums.  BWD=false: (x) -> sum x, sum x^2.  BWD=true: (x, dy, stats, gamma, beta) -> sum dz, sum dz*xhat
+// ---------------------------------------------------------------------------------------------------------------
+template <bool BWD, bool SILU>
+__global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                  const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
+                                  const bf16_t* __restrict__ beta, float* __restrict__ ws) {
+  extern __shared__ float red[];  // [RS][C][2]
+  const int TPR = C / 8;
+  const int RS = blockDim.x / TPR;
+  const int slot = threadIdx.x / TPR, cc = threadIdx.x - slot * TPR;
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunks = gridDim.x;
+  const int r0 = chunk * GN_ROWS, r1 = min(HW, r0 + GN_ROWS);
+  const int Cg = C / G;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  float mean[8], rstd[8], gm[8], bt[8];
+  if (BWD && slot < RS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cc * 8 + j, g = c / Cg;
+      mean[j] = stats[(b * G + g) * 2];
+      rstd[j] = stats[(b * G + g) * 2 + 1];
+      gm[j] = gamma ? bf2f(gamma[c]) : 1.f;
+      bt[j] = beta ? bf2f(beta[c]) : 0.f;
+    }
+  }
+  if (slot < RS) {
+    for (int r = r0 + slot; r < r1; r += RS) {
+      const size_t off = ((size_t)b * HW + r) * C + cc * 8;
+      float xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+      if (!BWD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s1[j] += xv[j];
+          s2[j] += xv[j] * xv[j];
+        }
+      } else {
+        float dv[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + off), dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mean[j]) * rstd[j];
+          float dz = dv[j];
+          if (SILU) {
+            const float z = xh * gm[j] + bt[j];
+            const float sg = sigmoidf_(z);
+            dz *= sg * (1.f + z * (1.f - sg));
+          }
+          s1[j] += dz;
+          s2[j] += dz * xh;
+        }
+      }
+    }
+  }
+  // reduce over slots through LDS
+  if (slot < RS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(slot * C + cc * 8 + j) * 2] = s1[j];
+      red[(slot * C + cc * 8 + j) * 2 + 1] = s2[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, q = 0.f;
+    for (int s = 0; s < RS; ++s) {
+      a += red[(s * C + c) * 2];
+      q += red[(s * C + c) * 2 + 1];
+    }
+    float* o = ws + (((size_t)b * nchunks + chunk) * C + c) * 2;
+    o[0] = a;
+    o[1] = q;
+  }
+}
+
+// one thread per (image, group).  FWD: stats = (mean, rstd).  BWD: coef = (mean(dz*gamma), mean(dz*gamma*xhat)).
+template <bool BWD>
+__global__ void gn_finalize_kernel(int B, int HW, int C, int G, int nchunks, float eps, const float* __restrict__ ws,
+                                   const bf16_t* __restrict__ gamma, float* __restrict__ out) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= B * G) return;
+  const int b = id / G, g = id - b * G;
+  const int Cg = C / G;
+  double a = 0.0, q = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    const float* p = ws + (((size_t)b * nchunks + k) * C + g * Cg) * 2;
+    for (int c = 0; c < Cg; ++c) {
+      const double gm = BWD ? (gamma ? (double)bf2f(gamma[g * Cg + c]) : 1.0) : 1.0;
+      a += gm * p[2 * c];
+      q += gm * p[2 * c + 1];
+    }
+  }
+  const double n = (double)HW * Cg;
+  if (!BWD) {
+    const double mean = a / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    out[id * 2] = (float)mean;
+    out[id * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+  } else {
+    out[id * 2] = (float)(a / n);
+    out[id * 2 + 1] = (float)(q / n);
+  }
+}
+
+// per-channel dgamma/dbeta from the bwd partials (sum over images and chunks)
+__global__ void gn_dparam_kernel(int B, int C, int nchunks, const float* __restrict__ ws, float* __restrict__ dgamma,
+                                 float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, q = 0.0;
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < nchunks; ++k) {
+      const float* p = ws + (((size_t)b * nchunks + k) * C + c) * 2;
+      a += p[0];
+      q += p[1];
+    }
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)a;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
+}
+
+template <bool SILU>
+__global__ void gn_apply_fwd_kernel(long nvec, int HW, int C, int G, const bf16_t* __restrict__ x,
+                                    const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
+                                    const bf16_t* __restrict__ beta, bf16_t* __restrict__ y) {
+  const int Cg = C / G, C8 = C / 8;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+    const long pix = v / C8;
+    const int c0 = (int)(v - pix * C8) * 8;
+    const int b = (int)(pix / HW);
+    float xv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j, g = c / Cg;
+      const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
+      float z = (xv[j] - mean) * rstd;
+      z = z * (gamma ? bf2f(gamma[c]) : 1.f) + (beta ? bf2f(beta[c]) : 0.f);
+      o[j] = SILU ? z * sigmoidf_(z) : z;
+    }
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8(o);
+  }
+}
+
+template <bool SILU>
+__global__ void gn_apply_bwd_kernel(long nvec, int HW, int C, int G, const bf16_t* __restrict__ x,
+                                    const bf16_t* __restrict__ dy, const float* __restrict__ stats,
+                                    const float* __restrict__ coef, const bf16_t* __restrict__ gamma,
+                                    const bf16_t* __restrict__ beta, const bf16_t* __restrict__ dadd,
+                                    bf16_t* __restrict__ dx) {
+  const int Cg = C / G, C8 = C / 8;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+    const long pix = v / C8;
+    const int c0 = (int)(v - pix * C8) * 8;
+    const int b = (int)(pix / HW);
+    float xv[8], dv[8], o[8], av[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), dv);
+    if (dadd) unpack8(*reinterpret_cast<const uint4*>(dadd + v * 8), av);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j, g = c / Cg;
+      const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
+      const float ca = coef[(b * G + g) * 2], cb = coef[(b * G + g) * 2 + 1];
+      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
+      const float xh = (xv[j] - mean) * rstd;
+      float dz = dv[j];
+      if (SILU) {
+        const float z = xh * gm + (beta ? bf2f(beta[c]) : 0.f);
+        const float sg = sigmoidf_(z);
+        dz *= sg * (1.f + z * (1.f - sg));
+      }
+      o[j] = rstd * (dz * gm - ca - xh * cb) + (dadd ? av[j] : 0.f);
+    }
+    *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
+  }
+}
+
+static int gn_block(int C) {
+  const int TPR = C / 8;
+  int rs = 1;
+  while (TPR * rs * 2 <= 512) rs *= 2;
+  return TPR * rs;
+}
+
+static int grid_ew(long nvec) {
+  long g = (nvec + 255) / 256;
+  if (g > 4096) g = 4096;
+  return (int)(g < 1 ? 1 : g);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// LayerNorm over the last dim (one wave per row).  MAXV = 16-B chunks per lane (C <= 64*8*MAXV).
+// ---------------------------------------------------------------------------------------------------------------
+template <int MAXV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int C, float eps, const bf16_t* __restrict__ x, long ldx,
+                                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                                     bf16_t* __restrict__ y, long ldy, float* __restrict__ stats) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int C8 = C / 8;
+  float v[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < C8) {
+      unpack8(*reinterpret_cast<const uint4*>(x + row * ldx + ch * 8), v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    }
+  }
+  const float mean = warp_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < C8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < C8) {
+      const uint4 gv = *reinterpret_cast<const uint4*>(gamma + ch * 8);
+      const uint4 bv = *reinterpret_cast<const uint4*>(beta + ch * 8);
+      float gf[8], bf[8], o[8];
+      unpack8(gv, gf);
+      unpack8(bv, bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * gf[j] + bf[j];
+      *reinterpret_cast<uint4*>(y + row * ldy + ch * 8) = pack8(o);
+    }
+  }
+  if (stats && lane == 0) {
+    stats[row * 2] = mean;
+    stats[row * 2 + 1] = rstd;
+  }
+}
+
+template <int MAXV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int C, const bf16_t* __restrict__ x, long ldx,
+                                                     const bf16_t* __restrict__ dy, long lddy,
+                                                     const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
+                                                     const bf16_t* __restrict__ dadd, long ldadd,
+                                                     bf16_t* __restrict__ dx, long lddx) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int C8 = C / 8;
+  const float mean = stats[row * 2], rstd = stats[row * 2 + 1];
+  float xh[MAXV][8], g[MAXV][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < C8) {
+      float xv[8], dv[8], gf[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + row * ldx + ch * 8), xv);
+      unpack8(*reinterpret_cast<const uint4*>(dy + row * lddy + ch * 8), dv);
+      unpack8(*reinterpret_cast<const uint4*>(gamma + ch * 8), gf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[i][j] = (xv[j] - mean) * rstd;
+        g[i][j] = dv[j] * gf[j];
+        s1 += g[i][j];
+        s2 += g[i][j] * xh[i][j];
+      }
+    }
+  }
+  const float a = warp_sum(s1) / C, b = warp_sum(s2) / C;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < C8) {
+      float o[8], av[8];
+      if (dadd) unpack8(*reinterpret_cast<const uint4*>(dadd + row * ldadd + ch * 8), av);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rstd * (g[i][j] - a - xh[i][j] * b) + (dadd ? av[j] : 0.f);
+      *reinterpret_cast<uint4*>(dx + row * lddx + ch * 8) = pack8(o);
+    }
+  }
+}
+
+extern "C" {
+
+size_t pso_group_norm_ws_bytes(int B, int HW, int C) {
+  return (size_t)B * cdiv(HW, GN_ROWS) * C * 2 * sizeof(float);
+}
+
+int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, const void* gamma, const void* beta,
+                       int silu, void* y, float* stats, void* ws, size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(B > 0 && HW > 0 && C > 0 && G > 0 && C % G == 0 && C % 8 == 0 && C <= 4096,
+                "pso_group_norm_fwd: bad shape B=%d HW=%d C=%d G=%d", B, HW, C, G);
+  PSO_ARG_CHECK(x && y && stats && ws, "pso_group_norm_fwd: null pointer");
+  PSO_ARG_CHECK(ws_bytes >= pso_group_norm_ws_bytes(B, HW, C), "pso_group_norm_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunks = cdiv(HW, GN_ROWS);
+  const int threads = gn_block(C);
+  const size_t shm = (size_t)(threads / (C / 8)) * C * 2 * sizeof(float);
+  gn_partial_kernel<false, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, (const bf16_t*)x, nullptr,
+                                                                          nullptr, nullptr, nullptr, (float*)ws);
+  gn_finalize_kernel<false><<<cdiv(B * G, 128), 128, 0, st>>>(B, HW, C, G, nchunks, eps, (const float*)ws, nullptr,
+                                                              stats);
+  const long nvec = (long)B * HW * C / 8;
+  if (silu)
+    gn_apply_fwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, (const bf16_t*)x, stats,
+                                                             (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y);
+  else
+    gn_apply_fwd_kernel<false><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, (const bf16_t*)x, stats,
+                                                              (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y);
+  return pso_check_launch("pso_group_norm_fwd");
+}
+
+int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* dy, const float* stats,
+                       const void* gamma, const void* beta, int silu, const void* dadd, void* dx, float* dgamma,
+                       float* dbeta, int accumulate_dparams, void* ws, size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(B > 0 && HW > 0 && C > 0 && G > 0 && C % G == 0 && C % 8 == 0 && C <= 4096,
+                "pso_group_norm_bwd: bad shape");
+  PSO_ARG_CHECK(x && dy && stats && dx && ws, "pso_group_norm_bwd: null pointer");
+  PSO_ARG_CHECK(ws_bytes >= pso_group_norm_ws_bytes(B, HW, C) + (size_t)B * G * 2 * sizeof(float),
+                "pso_group_norm_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunks = cdiv(HW, GN_ROWS);
+  const int threads = gn_block(C);
+  const size_t shm = (size_t)(threads / (C / 8)) * C * 2 * sizeof(float);
+  float* part = (float*)ws;
+  float* coef = (float*)((char*)ws + pso_group_norm_ws_bytes(B, HW, C));
+  const bf16_t *xp = (const bf16_t*)x, *dyp = (const bf16_t*)dy, *gp = (const bf16_t*)gamma,
+               *bp = (const bf16_t*)beta;
+  if (silu)
+    gn_partial_kernel<true, true><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part);
+  else
+    gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part);
+  gn_finalize_kernel<true><<<cdiv(B * G, 128), 128, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, gp, coef);
+  if (dgamma || dbeta)
+    gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part, dgamma, dbeta, accumulate_dparams);
+  const long nvec = (long)B * HW * C / 8;
+  if (silu)
+    gn_apply_bwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, xp, dyp, stats, coef, gp, bp,
+                                                             (const bf16_t*)dadd, (bf16_t*)dx);
+  else
+    gn_apply_bwd_kernel<false><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, xp, dyp, stats, coef, gp, bp,
+                                                              (const bf16_t*)dadd, (bf16_t*)dx);
+  return pso_check_launch("pso_group_norm_bwd");
+}
+
+int pso_layer_norm_fwd(int M, int C, float eps, const void* x, long ldx, const void* gamma, const void* beta, void* y,
+                       long ldy, float* stats, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && C > 0 && C % 8 == 0 && C <= 64 * 8 * 4, "pso_layer_norm_fwd: C=%d unsupported", C);
+  PSO_ARG_CHECK(x && y && gamma && beta, "pso_layer_norm_fwd: null pointer");
+  if (M == 0) return PSO_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int C8 = C / 8;
+  const int grid = cdiv(M, 4);
+  if (C8 <= 64)
+    ln_fwd_kernel<1><<<grid, 256, 0, st>>>(M, C, eps, (const bf16_t*)x, ldx, (const bf16_t*)gamma,
+                                          (const bf16_t*)beta, (bf16_t*)y, ldy, stats);
+  else if (C8 <= 128)
+    ln_fwd_kernel<2><<<grid, 256, 0, st>>>(M, C, eps, (const bf16_t*)x, ldx, (const bf16_t*)gamma,
+                                          (const bf16_t*)beta, (bf16_t*)y, ldy, stats);
+  else
+    ln_fwd_kernel<4><<<grid, 256, 0, st>>>(M, C, eps, (const bf16_t*)x, ldx, (const bf16_t*)gamma,
+                                          (const bf16_t*)beta, (bf16_t*)y, ldy, stats);
+  return pso_check_launch("pso_layer_norm_fwd");
+}
+
+int pso_layer_norm_bwd(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                       const void* gamma, const void* dadd, long ldadd, void* dx, long lddx, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && C > 0 && C % 8 == 0 && C <= 64 * 8 * 4, "pso_layer_norm_bwd: C=%d unsupported", C);
+  PSO_ARG_CHECK(x && dy && stats && gamma && dx, "pso_layer_norm_bwd: null pointer");
+  if (M == 0) return PSO_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int C8 = C / 8;
+  const int grid = cdiv(M, 4);
+  if (C8 <= 64)
+    ln_bwd_kernel<1><<<grid, 256, 0, st>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
+                                          (const bf16_t*)gamma, (const bf16_t*)dadd, ldadd, (bf16_t*)dx, lddx);
+  else if (C8 <= 128)
+    ln_bwd_kernel<2><<<grid, 256, 0, st>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
+                                          (const bf16_t*)gamma, (const bf16_t*)dadd, ldadd, (bf16_t*)dx, lddx);
+  else
+    ln_bwd_kernel<4><<<grid, 256, 0, st>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
+                                          (const bf16_t*)gamma, (const bf16_t*)dadd, ldadd, (bf16_t*)dx, lddx);
+  return pso_check_launch("pso_layer_norm_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+"""Thin Python wrappers over the libpso_amd C-ABI (one function per entry point of include/pso_amd.h).
+
+Tensors are plain torch device tensors used as memory; every computation happens in the HIP library.  Activations
+are channels-last bf16: linear inputs are [tokens, C] (any 2-D row-strided view), images are NHWC [B, H, W, C].
+There is no CPU / eager fallback: a missing library or a host tensor raises PsoLibError.
+"""
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, require_cuda, stream_ptr, dtype_code, PSO_BF16, PSO_F32
+
+CONV_NORMAL, CONV_UP2, CONV_T2 = 1, 2, 3
+BF16 = torch.bfloat16
+
+
+def _row_stride(t):
+    assert t.dim() == 2 and t.stride(1) == 1, "operand must be a 2-D view with contiguous rows"
+    return t.stride(0)
+
+
+def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=None, rows_per_group=1, out=None,
+         out_dtype=BF16, accumulate=False):
+    """out[M,N] = alpha*(a @ w^T + a2 @ w2^T) + bias + rowbias[m // rows_per_group] + resid."""
+    require_cuda(a, w)
+    M, K1 = a.shape
+    N = w.shape[0]
+    assert w.shape[1] == K1 and a.dtype == BF16 and w.dtype == BF16
+    K2 = 0
+    if a2 is not None:
+        K2 = a2.shape[1]
+        assert w2.shape == (N, K2) and a2.shape[0] == M
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype)
+    check(lib().pso_gemm(M, N, ptr(a), _row_stride(a), K1, ptr(w), _row_stride(w),
+                         ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
+                         ptr(w2), _row_stride(w2) if w2 is not None else 0,
+                         float(alpha), ptr(bias), ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
+                         int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
+                         ptr(out), _row_stride(out), dtype_code(out), int(accumulate), stream_ptr()), "pso_gemm")
+    return out
+
+
+def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=None, bias=None, rowbias=None,
+           resid=None, a2=None, w2=None, alpha=1.0, out=None, out_dtype=BF16, accumulate=False):
+    """NHWC implicit-GEMM conv.  x [B,H,W,C1] (+ x2 [B,H,W,C2] concatenated on channels); weight [Cout,ks,ks,C1+C2].
+    Returns [B,Ho,Wo,Cout]."""
+    require_cuda(x, weight)
+    B, H, W, C1 = x.shape
+    C2 = x2.shape[3] if x2 is not None else 0
+    Cout, ks, ks2, Ct = weight.shape
+    assert ks == ks2 and Ct == C1 + C2 and x.is_contiguous() and weight.is_contiguous()
+    if pad is None:
+        pad = ks // 2
+    if out_hw is None:
+        if mode == CONV_UP2:
+            out_hw = (2 * H, 2 * W)
+        elif mode == CONV_T2:
+            out_hw = (2 * H, 2 * W)
+        else:
+            out_hw = ((H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1)
+    Ho, Wo = out_hw
+    if out is None:
+        out = torch.empty((B, Ho, Wo, Cout), device=x.device, dtype=out_dtype)
+    K2 = a2.shape[1] if a2 is not None else 0
+    o2 = out.view(B * Ho * Wo, -1) if out.is_contiguous() else None
+    ldo = Cout if o2 is None else o2.stride(0)
+    check(lib().pso_conv2d(mode, B, ptr(x), C1, ptr(x2), C2, H, W, Ho, Wo, ks, stride, pad, ptr(weight), Cout,
+                           ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
+                           ptr(w2), _row_stride(w2) if w2 is not None else 0, float(alpha), ptr(bias),
+                           ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
+                           ptr(resid), Cout if resid is not None else 0, ptr(out), ldo, dtype_code(out),
+                           int(accumulate), stream_ptr()), "pso_conv2d")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# PSO step / loss
+# ------------------------------------------------------------------------------------------------------------------
+def step_logprob(mode, sample, eps, coef, prev=None, noise=None, noise_shared=False):
+    """One scheduler step + Gaussian log-prob.  sample/prev/noise fp32 [B, ...]; eps fp32|bf16; coef [B, 8]."""
+    require_cuda(sample, eps, coef, prev, noise)
+    B = sample.shape[0]
+    n = sample[0].numel()
+    sample = sample.contiguous()
+    eps = eps.contiguous()
+    lp = torch.empty(B, device=sample.device, dtype=torch.float32)
+    prev_out = None if prev is not None else torch.empty_like(sample, dtype=torch.float32)
+    ws_bytes = lib().pso_step_logprob_ws_bytes(B, n)
+    ws = torch.empty(ws_bytes, device=sample.device, dtype=torch.uint8)
+    check(lib().pso_step_logprob(mode, B, n, ptr(sample), ptr(eps), dtype_code(eps),
+                                 ptr(prev.contiguous()) if prev is not None else None,
+                                 ptr(noise.contiguous()) if noise is not None else None, int(noise_shared),
+                                 ptr(coef.contiguous()), ptr(prev_out), ptr(lp), ptr(ws), ws_bytes, stream_ptr()),
+          "pso_step_logprob")
+    return (prev if prev is not None else prev_out), lp
+
+
+def pair_loss_ws(P, n, device):
+    return torch.empty(lib().pso_pair_loss_ws_bytes(P, n), device=device, dtype=torch.uint8)
+
+
+def pair_loss_fwd(mode, x, x_prev, eps_pol, eps_ref, coef, pref, beta, clip_eps, ws):
+    P = x.shape[0] // 2
+    n = x[0].numel()
+    lp = torch.empty((2 * P, 2), device=x.device, dtype=torch.float32)
+    loss = torch.empty((), device=x.device, dtype=torch.float32)
+    check(lib().pso_pair_loss_fwd(mode, P, n, ptr(x), ptr(x_prev), ptr(eps_pol), ptr(eps_ref), dtype_code(eps_pol),
+                                  ptr(coef), ptr(pref), float(beta), float(clip_eps), ptr(lp), ptr(loss), ptr(ws),
+                                  ws.numel(), stream_ptr()), "pso_pair_loss_fwd")
+    return loss, lp
+
+
+def pair_loss_bwd(mode, x, x_prev, eps_pol, coef, pref, beta, clip_eps, ws, grad_out=None, grad_scale=1.0,
+                  out_dtype=BF16):
+    P = x.shape[0] // 2
+    n = x[0].numel()
+    deps = torch.empty(eps_pol.shape, device=x.device, dtype=out_dtype)
+    check(lib().pso_pair_loss_bwd(mode, P, n, ptr(x), ptr(x_prev), ptr(eps_pol), dtype_code(eps_pol), ptr(coef),
+                                  ptr(pref), float(beta), float(clip_eps), ptr(grad_out), float(grad_scale),
+                                  ptr(deps), dtype_code(deps), ptr(ws), ws.numel(), stream_ptr()),
+          "pso_pair_loss_bwd")
+    return deps
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Norms
+# ------------------------------------------------------------------------------------------------------------------
+def group_norm_fwd(x, gamma, beta, groups, eps, silu):
+    """x NHWC [B,H,W,C] (or [B,HW,C]) bf16 -> (y, stats[B,G,2])."""
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    y = torch.empty_like(x)
+    stats = torch.empty((B, groups, 2), device=x.device, dtype=torch.float32)
+    wsb = lib().pso_group_norm_ws_bytes(B, HW, C)
+    ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
+    check(lib().pso_group_norm_fwd(B, HW, C, groups, float(eps), ptr(x), ptr(gamma), ptr(beta), int(silu), ptr(y),
+                                   ptr(stats), ptr(ws), wsb, stream_ptr()), "pso_group_norm_fwd")
+    return y, stats
+
+
+def group_norm_bwd(x, dy, stats, gamma, beta, silu, dadd=None, dgamma=None, dbeta=None, accumulate=False):
+    B, C = x.shape[0], x.shape[-1]
+    G = stats.shape[1]
+    HW = x.numel() // (B * C)
+    dx = torch.empty_like(x)
+    wsb = lib().pso_group_norm_ws_bytes(B, HW, C) + B * G * 2 * 4
+    ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
+    check(lib().pso_group_norm_bwd(B, HW, C, G, ptr(x), ptr(dy.contiguous()), ptr(stats), ptr(gamma), ptr(beta),
+                                   int(silu), ptr(dadd), ptr(dx), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(ws),
+                                   wsb, stream_ptr()), "pso_group_norm_bwd")
+    return dx
+
+
+def layer_norm_fwd(x, gamma, beta, eps):
+    """x [M, C] (row-strided view ok) -> (y [M,C], stats [M,2])."""
+    M, C = x.shape
+    y = torch.empty((M, C), device=x.device, dtype=x.dtype)
+    stats = torch.empty((M, 2), device=x.device, dtype=torch.float32)
+    check(lib().pso_layer_norm_fwd(M, C, float(eps), ptr(x), _row_stride(x), ptr(gamma), ptr(beta), ptr(y), C,
+                                   ptr(stats), stream_ptr()), "pso_layer_norm_fwd")
+    return y, stats
+
+
+def layer_norm_bwd(x, dy, stats, gamma, dadd=None):
+    M, C = x.shape
+    dx = torch.empty((M, C), device=x.device, dtype=x.dtype)
+    check(lib().pso_layer_norm_bwd(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats), ptr(gamma),
+                                   ptr(dadd), _row_stride(dadd) if dadd is not None else 0, ptr(dx), C,
+                                   stream_ptr()), "pso_layer_norm_bwd")
+    return dx
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Attention: q/k/v/o are [B, S, H*64] tensors (views with unit last stride)
+# ------------------------------------------------------------------------------------------------------------------
+def _bsd(t):
+    assert t.dim() == 3 and t.stride(2) == 1
+    return t.stride(1), t.stride(0)
+
+
+def attention_fwd(q, k, v, heads, scale=None, out=None):
+    B, Sq, C = q.shape
+    Sk = k.shape[1]
+    assert C == heads * 64
+    if scale is None:
+        scale = 64 ** -0.5
+    if out is None:
+        out = torch.empty((B, Sq, C), device=q.device, dtype=q.dtype)
+    lse = torch.empty((B, heads, Sq), device=q.device, dtype=torch.float32)
+    (ldq, sqb), (ldk, skb), (ldv, svb), (ldo, sob) = _bsd(q), _bsd(k), _bsd(v), _bsd(out)
+    check(lib().pso_attention_fwd(B, heads, Sq, Sk, ptr(q), ldq, sqb, ptr(k), ldk, skb, ptr(v), ldv, svb,
+                                  float(scale), ptr(out), ldo, sob, ptr(lse), stream_ptr()), "pso_attention_fwd")
+    return out, lse
+
+
+def attention_bwd(q, k, v, o, lse, do, heads, scale=None, dq=None, dk=None, dv=None):
+    B, Sq, C = q.shape
+    Sk = k.shape[1]
+    if scale is None:
+        scale = 64 ** -0.5
+    dq = torch.empty_like(q, memory_format=torch.contiguous_format) if dq is None else dq
+    dk = torch.empty((B, Sk, C), device=q.device, dtype=q.dtype) if dk is None else dk
+    dv = torch.empty((B, Sk, C), device=q.device, dtype=q.dtype) if dv is None else dv
+    if Sk <= 256:
+        assert dk.stride(0) == Sk * dk.stride(1) and dv.stride(0) == Sk * dv.stride(1)
+    wsb = lib().pso_attention_bwd_ws_bytes(B, heads, Sq, Sk)
+    ws = torch.empty(wsb, device=q.device, dtype=torch.uint8)
+    do = do.contiguous()
+    a = [_bsd(t) for t in (q, k, v, o, do, dq, dk, dv)]
+    check(lib().pso_attention_bwd(B, heads, Sq, Sk, ptr(q), *a[0], ptr(k), *a[1], ptr(v), *a[2], ptr(o), *a[3],
+                                  ptr(lse), ptr(do), *a[4], float(scale), ptr(dq), *a[5], ptr(dk), *a[6], ptr(dv),
+                                  *a[7], ptr(ws), wsb, stream_ptr()), "pso_attention_bwd")
+    return dq, dk, dv
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Element-wise
+# ------------------------------------------------------------------------------------------------------------------
+def geglu_fwd(h):
+    M, F2 = h.shape
+    F = F2 // 2
+    out = torch.empty((M, F), device=h.device, dtype=h.dtype)
+    check(lib().pso_geglu_fwd(M, F, ptr(h), _row_stride(h), ptr(out), F, stream_ptr()), "pso_geglu_fwd")
+    return out
+
+
+def geglu_bwd(h, dout):
+    M, F2 = h.shape
+    F = F2 // 2
+    din = torch.empty((M, F2), device=h.device, dtype=h.dtype)
+    check(lib().pso_geglu_bwd(M, F, ptr(h), _row_stride(h), ptr(dout), _row_stride(dout), ptr(din), F2,
+                              stream_ptr()), "pso_geglu_bwd")
+    return din
+
+
+def silu(x):
+    y = torch.empty_like(x)
+    check(lib().pso_silu(x.numel(), ptr(x.contiguous()), ptr(y), stream_ptr()), "pso_silu")
+    return y
+
+
+def timestep_embedding(t, dim, out=None, out_col=0):
+    t = t.reshape(-1).float().contiguous()
+    if out is None:
+        out = torch.empty((t.shape[0], dim), device=t.device, dtype=BF16)
+    check(lib().pso_timestep_embedding(t.shape[0], dim, ptr(t), ptr(out), out.stride(0), out_col, stream_ptr()),
+          "pso_timestep_embedding")
+    return out
+
+
+def transpose(x, out=None):
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C, R), device=x.device, dtype=x.dtype)
+    check(lib().pso_transpose(R, C, ptr(x), _row_stride(x), ptr(out), _row_stride(out), stream_ptr()),
+          "pso_transpose")
+    return out
+
+
+def im2col3(x, kp):
+    B, H, W, C = x.shape
+    out = torch.empty((B * H * W, kp), device=x.device, dtype=x.dtype)
+    check(lib().pso_im2col3(B, H, W, C, ptr(x.contiguous()), ptr(out), kp, stream_ptr()), "pso_im2col3")
+    return out
+
+
+def sumpool2(x, dadd=None):
+    B, H2, W2, C = x.shape
+    out = torch.empty((B, H2 // 2, W2 // 2, C), device=x.device, dtype=x.dtype)
+    check(lib().pso_sumpool2(B, H2 // 2, W2 // 2, C, ptr(x.contiguous()), ptr(dadd), ptr(out), stream_ptr()),
+          "pso_sumpool2")
+    return out
+
+
+def axpby(a, x, b=0.0, z=None, out=None):
+    out = torch.empty_like(x) if out is None else out
+    check(lib().pso_axpby(x.numel(), float(a), ptr(x.contiguous()), float(b),
+                          ptr(z.contiguous()) if z is not None else None, ptr(out), stream_ptr()), "pso_axpby")
+    return out
+
+
+def add(x, z):
+    return axpby(1.0, x, 1.0, z)
+
+
+def cast_f32_bf16(x, scale=1.0, out=None):
+    out = torch.empty(x.shape, device=x.device, dtype=BF16) if out is None else out
+    check(lib().pso_cast_f32_bf16(x.numel(), ptr(x.contiguous()), float(scale), ptr(out), stream_ptr()),
+          "pso_cast_f32_bf16")
+    return out
+
+
+def cast_bf16_f32(x, out=None):
+    out = torch.empty(x.shape, device=x.device, dtype=torch.float32) if out is None else out
+    check(lib().pso_cast_bf16_f32(x.numel(), ptr(x.contiguous()), ptr(out), stream_ptr()), "pso_cast_bf16_f32")
+    return out
+
+
+def conv_weight_t(w, flip):
+    """[Co,k,k,Ci] -> [Ci,k,k,Co] (flip rotates the taps)."""
+    Co, ks, _, Ci = w.shape
+    out = torch.empty((Ci, ks, ks, Co), device=w.device, dtype=w.dtype)
+    check(lib().pso_conv_weight_t(Co, ks, Ci, int(flip), ptr(w.contiguous()), ptr(out), stream_ptr()),
+          "pso_conv_weight_t")
+    return out

@@ -1,0 +1,108 @@
+"""GPU parity of the GEMM / conv kernels against a plain torch fp32 reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 320, 640), (77, 1280, 2048), (4100, 640, 640),
+                                   (1024, 10240, 1280), (5, 1280, 2816), (300, 4, 72), (1000, 3, 128)])
+def test_gemm_vs_fp32(cuda, M, N, K):
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda, generator=g).bfloat16()
+    r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    out = K_.gemm(a, w, bias=b, resid=r, alpha=0.5)
+    ref = 0.5 * (a.float() @ w.float().t()) + b.float() + r.float()
+    assert _rel(out, ref) < 4e-3
+    out32 = K_.gemm(a, w, out_dtype=torch.float32)
+    assert _rel(out32, a.float() @ w.float().t()) < 1e-5
+
+
+def test_gemm_lora_tail_and_accumulate(cuda):
+    from pairwise_sample_optimization_amd import kernels as K_
+    M, N, K, r = 640, 640, 640, 32
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / 25).bfloat16()
+    u = torch.randn(M, r, device=cuda).bfloat16()
+    wb = (torch.randn(N, r, device=cuda) / 6).bfloat16()
+    out = K_.gemm(a, w, a2=u, w2=wb, out_dtype=torch.float32)
+    ref = a.float() @ w.float().t() + u.float() @ wb.float().t()
+    assert _rel(out, ref) < 1e-5
+    K_.gemm(a, w, out=out, out_dtype=torch.float32, accumulate=True)
+    assert _rel(out, ref + a.float() @ w.float().t()) < 1e-5
+    # strided operand views (sub-columns of a wider buffer)
+    big = torch.randn(M, 3 * K, device=cuda).bfloat16()
+    o2 = K_.gemm(big[:, K:2 * K], w)
+    assert _rel(o2, big[:, K:2 * K].float() @ w.float().t()) < 4e-3
+    # rowbias grouped rows (time-embedding add)
+    rb = torch.randn(5, N, device=cuda).bfloat16()
+    o3 = K_.gemm(a, w, rowbias=rb, rows_per_group=128, out_dtype=torch.float32)
+    ref3 = a.float() @ w.float().t() + rb.float().repeat_interleave(128, 0)
+    assert _rel(o3, ref3) < 1e-5
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("B,C1,C2,H,Cout,ks,stride", [(2, 64, 0, 16, 128, 3, 1), (1, 320, 0, 32, 320, 3, 1),
+                                                       (2, 128, 64, 16, 64, 3, 1), (2, 128, 0, 16, 128, 3, 2),
+                                                       (2, 128, 192, 8, 64, 1, 1), (1, 64, 0, 9, 4, 3, 1)])
+def test_conv_normal(cuda, B, C1, C2, H, Cout, ks, stride):
+    from pairwise_sample_optimization_amd import kernels as K_
+    x = torch.randn(B, C1 + C2, H, H, device=cuda).bfloat16()
+    w = (torch.randn(Cout, C1 + C2, ks, ks, device=cuda) / (ks * (C1 + C2) ** 0.5)).bfloat16()
+    bias = torch.randn(Cout, device=cuda).bfloat16()
+    temb = torch.randn(B, Cout, device=cuda).bfloat16()
+    ref = F.conv2d(x.float(), w.float(), bias.float(), stride=stride, padding=ks // 2) + temb.float()[:, :, None, None]
+    xh = _nhwc(x)
+    x1, x2 = xh[..., :C1].contiguous(), (xh[..., C1:].contiguous() if C2 else None)
+    out = K_.conv2d(x1, _nhwc(w), x2=x2, stride=stride, bias=bias, rowbias=temb, out_dtype=torch.float32)
+    assert _rel(_nchw(out), ref) < 1e-5
+
+
+def test_conv_up2(cuda):
+    from pairwise_sample_optimization_amd import kernels as K_
+    x = torch.randn(2, 128, 8, 8, device=cuda).bfloat16()
+    w = (torch.randn(64, 128, 3, 3, device=cuda) / 30).bfloat16()
+    ref = F.conv2d(F.interpolate(x.float(), scale_factor=2.0, mode="nearest"), w.float(), padding=1)
+    out = K_.conv2d(_nhwc(x), _nhwc(w), mode=K_.CONV_UP2, out_dtype=torch.float32)
+    assert _rel(_nchw(out), ref) < 1e-5
+
+
+def test_conv_t2_is_stride2_input_grad(cuda):
+    from pairwise_sample_optimization_amd import kernels as K_
+    B, Ci, Co, H = 2, 64, 128, 16
+    x = torch.randn(B, Ci, H, H, device=cuda, requires_grad=True)
+    w = (torch.randn(Co, Ci, 3, 3, device=cuda) / 30).bfloat16().float()
+    y = F.conv2d(x, w, stride=2, padding=1)
+    dy = torch.randn_like(y).bfloat16().float()
+    (gx,) = torch.autograd.grad(y, x, dy)
+    wt = w.permute(1, 2, 3, 0).contiguous().bfloat16()  # [Ci][kh][kw][Co], unflipped
+    out = K_.conv2d(_nhwc(dy.bfloat16()), wt, mode=K_.CONV_T2, out_hw=(H, H), out_dtype=torch.float32)
+    assert _rel(_nchw(out), gx) < 1e-5
+
+
+def test_conv_stride1_input_grad_flipped(cuda):
+    from pairwise_sample_optimization_amd import kernels as K_
+    B, Ci, Co, H = 2, 64, 128, 16
+    x = torch.randn(B, Ci, H, H, device=cuda, requires_grad=True)
+    w = (torch.randn(Co, Ci, 3, 3, device=cuda) / 30).bfloat16().float()
+    y = F.conv2d(x, w, padding=1)
+    dy = torch.randn_like(y).bfloat16().float()
+    (gx,) = torch.autograd.grad(y, x, dy)
+    wf = w.flip(2, 3).permute(1, 2, 3, 0).contiguous().bfloat16()  # [Ci][kh'][kw'][Co]
+    out = K_.conv2d(_nhwc(dy.bfloat16()), wf, out_dtype=torch.float32)
+    assert _rel(_nchw(out), gx) < 1e-5

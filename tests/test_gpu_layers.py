@@ -1,0 +1,126 @@
+"""GPU parity of norm / attention / element-wise kernels (fwd + bwd) against plain torch fp32 references."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("B,HW,C,silu", [(2, 256, 320, True), (2, 64, 640, False), (1, 1024, 1280, True),
+                                          (2, 4096, 128, True), (1, 100, 2560, False)])
+def test_group_norm_fwd_bwd(cuda, B, HW, C, silu):
+    from pairwise_sample_optimization_amd import kernels as K
+    x = (torch.randn(B, HW, C, device=cuda) * 2 + 0.5).bfloat16()
+    gm = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
+    bt = (0.1 * torch.randn(C, device=cuda)).bfloat16()
+    xr = x.float().permute(0, 2, 1).requires_grad_(True)  # [B,C,HW]
+    ref = F.group_norm(xr, 32, gm.float(), bt.float(), eps=1e-5)
+    if silu:
+        ref = F.silu(ref)
+    y, st = K.group_norm_fwd(x, gm, bt, 32, 1e-5, silu)
+    assert _rel(y.permute(0, 2, 1), ref) < 8e-3
+    dy = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(ref, xr, dy.float().permute(0, 2, 1))
+    dadd = torch.randn_like(x)
+    dg = torch.zeros(C, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    dx = K.group_norm_bwd(x, dy, st, gm, bt, silu, dadd=dadd, dgamma=dg, dbeta=db)
+    assert _rel(dx.permute(0, 2, 1), gx + dadd.float().permute(0, 2, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("M,C", [(300, 640), (77, 1280), (1024, 320), (64, 2048)])
+def test_layer_norm_fwd_bwd(cuda, M, C):
+    from pairwise_sample_optimization_amd import kernels as K
+    x = (torch.randn(M, C, device=cuda) + 0.3).bfloat16()
+    gm = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
+    bt = (0.1 * torch.randn(C, device=cuda)).bfloat16()
+    xr = x.float().requires_grad_(True)
+    ref = F.layer_norm(xr, (C,), gm.float(), bt.float(), 1e-5)
+    y, st = K.layer_norm_fwd(x, gm, bt, 1e-5)
+    assert _rel(y, ref) < 8e-3
+    dy = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(ref, xr, dy.float())
+    dx = K.layer_norm_bwd(x, dy, st, gm)
+    assert _rel(dx, gx) < 1e-2
+
+
+def _attn_ref(q, k, v, H):
+    B, Sq, C = q.shape
+    f = lambda t: t.float().reshape(B, t.shape[1], H, 64).transpose(1, 2)
+    o = F.scaled_dot_product_attention(f(q), f(k), f(v))
+    return o.transpose(1, 2).reshape(B, Sq, C)
+
+
+@pytest.mark.parametrize("B,H,Sq,Sk", [(2, 2, 256, 256), (1, 10, 4096, 4096), (2, 5, 300, 77), (1, 4, 128, 1000),
+                                        (2, 20, 1024, 1024), (1, 2, 100, 100)])
+def test_attention_fwd_bwd(cuda, B, H, Sq, Sk):
+    from pairwise_sample_optimization_amd import kernels as K
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(Sq + Sk)
+    # q/k/v as column slices of a fused projection output, like the UNet does
+    qkv = torch.randn(B, Sq, 3 * C, device=cuda, generator=g).bfloat16()
+    q = qkv[..., :C]
+    if Sk == Sq:
+        k, v = qkv[..., C:2 * C], qkv[..., 2 * C:]
+    else:
+        kv = torch.randn(B, Sk, 2 * C, device=cuda, generator=g).bfloat16()
+        k, v = kv[..., :C], kv[..., C:]
+    o, lse = K.attention_fwd(q, k, v, H)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, H)
+    assert _rel(o, ref) < 1e-2
+    do = torch.randn(B, Sq, C, device=cuda, generator=g).bfloat16()
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    dq, dk, dv = K.attention_bwd(q, k, v, o, lse, do, H)
+    assert _rel(dq, gq) < 2e-2
+    assert _rel(dk, gk) < 2e-2
+    assert _rel(dv, gv) < 2e-2
+
+
+def test_geglu_silu_temb(cuda):
+    from pairwise_sample_optimization_amd import kernels as K
+    h = torch.randn(300, 2 * 640, device=cuda).bfloat16()
+    hr = h.float().requires_grad_(True)
+    a, gt = hr.chunk(2, dim=-1)
+    ref = a * F.gelu(gt)
+    out = K.geglu_fwd(h)
+    assert _rel(out, ref) < 8e-3
+    d = torch.randn_like(out)
+    (g,) = torch.autograd.grad(ref, hr, d.float())
+    assert _rel(K.geglu_bwd(h, d), g) < 1e-2
+    x = torch.randn(4, 1280, device=cuda).bfloat16()
+    assert _rel(K.silu(x), F.silu(x.float())) < 8e-3
+    t = torch.tensor([999.0, 499.0, 0.0, 1024.0], device=cuda)
+    emb = K.timestep_embedding(t, 320)
+    half = 160
+    ex = torch.exp(-math.log(10000) * torch.arange(half, device=cuda, dtype=torch.float32) / half)
+    arg = t[:, None] * ex[None]
+    ref = torch.cat([torch.cos(arg), torch.sin(arg)], -1)
+    assert (emb.float() - ref).abs().max() < 1e-2
+
+
+def test_transpose_im2col_sumpool_weight_t(cuda):
+    from pairwise_sample_optimization_amd import kernels as K
+    x = torch.randn(300, 130, device=cuda).bfloat16()
+    assert torch.equal(K.transpose(x), x.t().contiguous())
+    img = torch.randn(2, 9, 7, 4, device=cuda).bfloat16()
+    cols = K.im2col3(img, 64)
+    w = torch.randn(8, 4, 3, 3, device=cuda).bfloat16()
+    ref = F.conv2d(img.float().permute(0, 3, 1, 2), w.float(), padding=1)
+    wk = torch.zeros(8, 64, device=cuda).bfloat16()
+    wk[:, :36] = w.permute(0, 2, 3, 1).reshape(8, 36)
+    out = K.gemm(cols, wk, out_dtype=torch.float32).reshape(2, 9, 7, 8).permute(0, 3, 1, 2)
+    assert _rel(out, ref) < 1e-5
+    u = torch.randn(2, 8, 6, 64, device=cuda).bfloat16()
+    sp = K.sumpool2(u)
+    refp = F.avg_pool2d(u.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4
+    assert _rel(sp, refp) < 8e-3
+    wt = torch.randn(16, 3, 3, 8, device=cuda).bfloat16()
+    assert torch.equal(K.conv_weight_t(wt, True), wt.flip(1, 2).permute(3, 1, 2, 0).contiguous())
+    assert torch.equal(K.conv_weight_t(wt, False), wt.permute(3, 1, 2, 0).contiguous())
