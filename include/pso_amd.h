@@ -91,11 +91,13 @@ int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_pre
  *           DP/sdxl_turbo_with_logprob.py:126-132, DP/sdxl_dmd_with_logprob.py:117-122.  The (A2, B2) pair is the
  *           LoRA up-projection fused as a K-tail; the same entry point computes the backward GEMMs (dX with W^T, dW).
  * All A/B operands are bf16 with K contiguous; K1, K2 multiples of 8; rows 16-B aligned.
+ * tail_group_n > 0 (multiple of 64): output columns [j*tail_group_n, (j+1)*tail_group_n) take their K2-tail from A2
+ * columns [j*K2, (j+1)*K2) -- three LoRA adapters (q, k, v) fused into one QKV projection with B2 = [3C][r].
  * ---------------------------------------------------------------------------------------------------------------- */
 int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
-             void* stream);
+             int tail_group_n, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).
@@ -158,7 +160,7 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
  *   silu: y = x * sigmoid(x)                                                 (time-embedding nonlinearity)
  *   timestep_embedding: t fp32 [n] -> out[:, out_col:out_col+dim] = [cos | sin](t * 10000^(-i/(dim/2)))
  *                                                       (diffusers Timesteps, flip_sin_to_cos=True, shift=0)
- *   transpose [R][C] -> [C][R]; im2col3 (3x3 pad 1, small C, zero padded to Kp columns); sumpool2 (2x2 sum, the
+ *   transpose [R][C] -> [C][Rp] (rows >= R read as 0: zero-padded GEMM reduction dims); im2col3 (3x3 pad 1, small C, zero padded to Kp columns); sumpool2 (2x2 sum, the
  *   input-gradient of nearest-2x upsample); axpby y = a*x + b*z; casts; conv_weight_t ([Co][k][k][Ci] ->
  *   [Ci][k][k][Co], flip=1 rotates the taps: the input-gradient weight of a stride-1 conv).
  * ---------------------------------------------------------------------------------------------------------------- */
@@ -167,13 +169,21 @@ int pso_geglu_bwd(long M, int F, const void* in, long ldi, const void* dout, lon
                   void* stream);
 int pso_silu(long n, const void* x, void* y, void* stream);
 int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, int out_col, void* stream);
-int pso_transpose(int R, int C, const void* in, long ldi, void* out, long ldo, void* stream);
+int pso_transpose(int R, int Rp, int C, const void* in, long ldi, void* out, long ldo, void* stream);
 int pso_im2col3(int B, int H, int W, int C, const void* in, void* out, int Kp, void* stream);
 int pso_sumpool2(int B, int H, int W, int C, const void* in, const void* dadd, void* out, void* stream);
 int pso_axpby(long n, float a, const void* x, float b, const void* z, void* y, void* stream);
 int pso_cast_f32_bf16(long n, const float* x, float scale, void* y, void* stream);
 int pso_cast_bf16_f32(long n, const void* x, float* y, void* stream);
 int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt, void* stream);
+/* channel concat of NHWC rows (torch.cat([h, skip], dim=1) of the up blocks) and its inverse; the split can add a
+ * second gradient into the skip part (the skip tensor also feeds the next down layer). */
+/* layout conversion of the (small) latent tensors at the diffusers NCHW API boundary */
+int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream);
+int pso_nhwc_to_nchw(int B, int C, long HW, const void* src, void* dst, int dst_dtype, void* stream);
+int pso_concat_channels(long npix, int C1, const void* x1, int C2, const void* x2, void* out, void* stream);
+int pso_split_channels(long npix, int C1, int C2, const void* in, void* y1, void* y2, const void* add2,
+                       void* stream);
 
 #ifdef __cplusplus
 }

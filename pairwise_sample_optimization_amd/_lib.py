@@ -37,7 +37,7 @@ SIGNATURES = {
     "pso_pair_loss_fwd": (ci, [ci, ci, ci, vp, vp, vp, vp, ci, vp, vp, cf, cf, vp, vp, vp, csz, vp]),
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
-                      vp]),
+                      ci, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),
     "pso_group_norm_ws_bytes": (csz, [ci, ci, ci]),
@@ -53,13 +53,17 @@ SIGNATURES = {
     "pso_geglu_bwd": (ci, [cl, ci, vp, cl, vp, cl, vp, cl, vp]),
     "pso_silu": (ci, [cl, vp, vp, vp]),
     "pso_timestep_embedding": (ci, [ci, ci, vp, vp, cl, ci, vp]),
-    "pso_transpose": (ci, [ci, ci, vp, cl, vp, cl, vp]),
+    "pso_transpose": (ci, [ci, ci, ci, vp, cl, vp, cl, vp]),
     "pso_im2col3": (ci, [ci, ci, ci, ci, vp, vp, ci, vp]),
     "pso_sumpool2": (ci, [ci, ci, ci, ci, vp, vp, vp, vp]),
     "pso_axpby": (ci, [cl, cf, vp, cf, vp, vp, vp]),
     "pso_cast_f32_bf16": (ci, [cl, vp, cf, vp, vp]),
     "pso_cast_bf16_f32": (ci, [cl, vp, vp, vp]),
     "pso_conv_weight_t": (ci, [ci, ci, ci, ci, vp, vp, vp]),
+    "pso_concat_channels": (ci, [cl, ci, vp, ci, vp, vp, vp]),
+    "pso_nchw_to_nhwc": (ci, [ci, ci, cl, vp, ci, vp, vp]),
+    "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),
+    "pso_split_channels": (ci, [cl, ci, ci, vp, vp, vp, vp, vp]),
 }
 
 

@@ -98,9 +98,9 @@ __global__ void timestep_embed_kernel(int n, int dim, const float* __restrict__ 
   }
 }
 
-// 32x32 tiled transpose, bf16: in [R][C] (ldi) -> out [C][R] (ldo)
-__global__ void transpose_kernel(int R, int C, const bf16_t* __restrict__ in, long ldi, bf16_t* __restrict__ out,
-                                 long ldo) {
+// 64x64 tiled transpose, bf16: in [R][C] (ldi) -> out [C][Rp] (ldo); rows R..Rp-1 of the input read as zero
+__global__ void transpose_kernel(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
+                                 bf16_t* __restrict__ out, long ldo) {
   __shared__ bf16_t tile[64][66];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
@@ -111,7 +111,7 @@ __global__ void transpose_kernel(int R, int C, const bf16_t* __restrict__ in, lo
   __syncthreads();
   for (int i = ty; i < 64; i += 4) {
     const int c = c0 + i, r = r0 + tx;
-    if (c < C && r < R) out[(long)c * ldo + r] = tile[tx][i];
+    if (c < C && r < Rp) out[(long)c * ldo + r] = tile[tx][i];
   }
 }
 
@@ -201,7 +201,98 @@ __global__ void conv_weight_t_kernel(int Co, int ks, int Ci, int flip, const bf1
   }
 }
 
+// out [npix][C1+C2] = [x1 | x2]  (torch.cat(dim=1) of NCHW == channel concat of NHWC rows)
+__global__ void concat_kernel(long npix, int C1, const bf16_t* __restrict__ x1, int C2, const bf16_t* __restrict__ x2,
+                              bf16_t* __restrict__ out) {
+  const int C8 = (C1 + C2) / 8, c18 = C1 / 8;
+  GRID_STRIDE(v, npix * C8) {
+    const long p = v / C8;
+    const int ch = (int)(v - p * C8);
+    const uint4 val = ch < c18 ? *reinterpret_cast<const uint4*>(x1 + p * C1 + ch * 8)
+                               : *reinterpret_cast<const uint4*>(x2 + p * C2 + (ch - c18) * 8);
+    *reinterpret_cast<uint4*>(out + v * 8) = val;
+  }
+}
+
+// inverse of concat, with optional accumulation of the second part into an existing gradient (d_skip += ...)
+__global__ void split_kernel(long npix, int C1, int C2, const bf16_t* __restrict__ in, bf16_t* __restrict__ y1,
+                             bf16_t* __restrict__ y2, const bf16_t* __restrict__ add2) {
+  const int C8 = (C1 + C2) / 8, c18 = C1 / 8;
+  GRID_STRIDE(v, npix * C8) {
+    const long p = v / C8;
+    const int ch = (int)(v - p * C8);
+    const uint4 val = *reinterpret_cast<const uint4*>(in + v * 8);
+    if (ch < c18) {
+      *reinterpret_cast<uint4*>(y1 + p * C1 + ch * 8) = val;
+    } else {
+      bf16_t* o = y2 + p * C2 + (ch - c18) * 8;
+      if (add2) {
+        float a[8], b[8];
+        unpack8e(val, a);
+        unpack8e(*reinterpret_cast<const uint4*>(add2 + p * C2 + (ch - c18) * 8), b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        *reinterpret_cast<uint4*>(o) = pack8e(a);
+      } else {
+        *reinterpret_cast<uint4*>(o) = val;
+      }
+    }
+  }
+}
+
+// NCHW (fp32 or bf16) -> NHWC bf16, and back (fp32 or bf16 out).  Small tensors (latents): plain element mapping.
+__global__ void nchw_to_nhwc_kernel(int B, int C, long HW, const void* __restrict__ src, int src_f32,
+                                    bf16_t* __restrict__ dst) {
+  GRID_STRIDE(i, (long)B * C * HW) {
+    const int c = (int)(i % C);
+    const long p = (i / C) % HW;
+    const int b = (int)(i / (C * HW));
+    const long s = ((long)b * C + c) * HW + p;
+    dst[i] = src_f32 ? f2bf(reinterpret_cast<const float*>(src)[s]) : reinterpret_cast<const bf16_t*>(src)[s];
+  }
+}
+__global__ void nhwc_to_nchw_kernel(int B, int C, long HW, const bf16_t* __restrict__ src, void* __restrict__ dst,
+                                    int dst_f32) {
+  GRID_STRIDE(i, (long)B * C * HW) {
+    const long p = i % HW;
+    const int c = (int)((i / HW) % C);
+    const int b = (int)(i / (C * HW));
+    const bf16_t v = src[((long)b * HW + p) * C + c];
+    if (dst_f32) reinterpret_cast<float*>(dst)[i] = bf2f(v);
+    else reinterpret_cast<bf16_t*>(dst)[i] = v;
+  }
+}
+
 extern "C" {
+
+int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream) {
+  PSO_ARG_CHECK(src && dst && (src_dtype == PSO_F32 || src_dtype == PSO_BF16), "pso_nchw_to_nhwc: bad args");
+  nchw_to_nhwc_kernel<<<grid_for((long)B * C * HW), 256, 0, (hipStream_t)stream>>>(B, C, HW, src,
+                                                                                  src_dtype == PSO_F32, (bf16_t*)dst);
+  return pso_check_launch("pso_nchw_to_nhwc");
+}
+
+int pso_nhwc_to_nchw(int B, int C, long HW, const void* src, void* dst, int dst_dtype, void* stream) {
+  PSO_ARG_CHECK(src && dst && (dst_dtype == PSO_F32 || dst_dtype == PSO_BF16), "pso_nhwc_to_nchw: bad args");
+  nhwc_to_nchw_kernel<<<grid_for((long)B * C * HW), 256, 0, (hipStream_t)stream>>>(B, C, HW, (const bf16_t*)src,
+                                                                                  dst, dst_dtype == PSO_F32);
+  return pso_check_launch("pso_nhwc_to_nchw");
+}
+
+int pso_concat_channels(long npix, int C1, const void* x1, int C2, const void* x2, void* out, void* stream) {
+  PSO_ARG_CHECK(C1 % 8 == 0 && C2 % 8 == 0 && x1 && x2 && out, "pso_concat_channels: C %% 8");
+  concat_kernel<<<grid_for(npix * (C1 + C2) / 8), 256, 0, (hipStream_t)stream>>>(
+      npix, C1, (const bf16_t*)x1, C2, (const bf16_t*)x2, (bf16_t*)out);
+  return pso_check_launch("pso_concat_channels");
+}
+
+int pso_split_channels(long npix, int C1, int C2, const void* in, void* y1, void* y2, const void* add2,
+                       void* stream) {
+  PSO_ARG_CHECK(C1 % 8 == 0 && C2 % 8 == 0 && in && y1 && y2, "pso_split_channels: C %% 8");
+  split_kernel<<<grid_for(npix * (C1 + C2) / 8), 256, 0, (hipStream_t)stream>>>(
+      npix, C1, C2, (const bf16_t*)in, (bf16_t*)y1, (bf16_t*)y2, (const bf16_t*)add2);
+  return pso_check_launch("pso_split_channels");
+}
 
 int pso_geglu_fwd(long M, int F, const void* in, long ldi, void* out, long ldo, void* stream) {
   PSO_ARG_CHECK(F % 8 == 0 && ldi % 8 == 0 && ldo % 8 == 0 && in && out, "pso_geglu_fwd: bad args");
@@ -233,10 +324,10 @@ int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, 
   return pso_check_launch("pso_timestep_embedding");
 }
 
-int pso_transpose(int R, int C, const void* in, long ldi, void* out, long ldo, void* stream) {
-  PSO_ARG_CHECK(in && out, "pso_transpose: null");
-  dim3 grid(cdiv(C, 64), cdiv(R, 64));
-  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(R, C, (const bf16_t*)in, ldi, (bf16_t*)out, ldo);
+int pso_transpose(int R, int Rp, int C, const void* in, long ldi, void* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(in && out && Rp >= R, "pso_transpose: bad args");
+  dim3 grid(cdiv(C, 64), cdiv(Rp, 64));
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(R, Rp, C, (const bf16_t*)in, ldi, (bf16_t*)out, ldo);
   return pso_check_launch("pso_transpose");
 }
 

@@ -36,6 +36,7 @@ struct GemmArgs {
   const bf16_t* b1; long ldb1;
   const bf16_t* a2; long lda2; int K2;
   const bf16_t* b2; long ldb2;
+  int tail_group_n;  // >0: the A2 tail of output columns [j*G, (j+1)*G) starts at A2 column j*K2
   int M, N;
   ConvGeom conv;
   float alpha;
@@ -119,6 +120,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
   const int nt1 = (g.K1 + BK - 1) / BK;
   const int nt2 = g.a2 ? (g.K2 + BK - 1) / BK : 0;
   const int nt = nt1 + nt2;
+  const long a2_off = g.tail_group_n > 0 ? (long)(n0 / g.tail_group_n) * g.K2 : 0;
 
   // staging coordinates: chunk q = tid + 256*i -> row q/8, k-chunk q%8
   RowCoord rc[T::A_CH];
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
     for (int i = 0; i < T::A_CH; ++i) {
       const int q = tid + GEMM_THREADS * i;
       const int row = q >> 3, kc = (q & 7) * 8;
-      if (second) ra[i] = load_chunk_dense(g.a2, g.lda2, m0 + row, g.M, k0 + kc, g.K2);
+      if (second) ra[i] = load_chunk_dense(g.a2 + a2_off, g.lda2, m0 + row, g.M, k0 + kc, g.K2);
       else if (CONV) ra[i] = load_chunk_conv(g, rc[i], k0 + kc);
       else ra[i] = load_chunk_dense(g.a1, g.lda1, m0 + row, g.M, k0 + kc, g.K1);
     }
@@ -274,6 +276,11 @@ static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
+  if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
+    pso_set_error("pso_gemm: tail_group_n must be a multiple of 64");
+    return PSO_ERR_ARG;
+  }
+  if (g.tail_group_n > 0 && (g.tail_group_n % 128) != 0) return launch<128, 64>(g, st);
   g.vec_ok = (g.ldo % 4) == 0 && (g.out_dtype == PSO_F32 ? al16(g.out) : al8(g.out)) &&
              (!g.resid || ((g.ldr % 4) == 0 && al8(g.resid))) && (!g.bias || al8(g.bias)) &&
              (!g.rowbias || (al8(g.rowbias) && (g.ld_rowbias % 4) == 0));
@@ -288,7 +295,7 @@ extern "C" {
 int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
-             void* stream) {
+             int tail_group_n, void* stream) {
   PSO_ARG_CHECK(M >= 0 && N >= 0 && K1 >= 0 && (K1 % 8) == 0, "pso_gemm: need K1 %% 8 == 0 (K1=%d)", K1);
   PSO_ARG_CHECK(a1 && b1 && out, "pso_gemm: null operand");
   PSO_ARG_CHECK(al16(a1) && al16(b1) && (lda1 % 8) == 0 && (ldb1 % 8) == 0, "pso_gemm: A1/B1 must be 16-B aligned rows");
@@ -302,6 +309,7 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
   g.b1 = (const bf16_t*)b1; g.ldb1 = ldb1;
   g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
   g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
+  g.tail_group_n = a2 ? tail_group_n : 0;
   g.M = M; g.N = N;
   g.alpha = alpha;
   g.bias = (const bf16_t*)bias;

@@ -19,16 +19,18 @@ def _row_stride(t):
 
 
 def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=None, rows_per_group=1, out=None,
-         out_dtype=BF16, accumulate=False):
-    """out[M,N] = alpha*(a @ w^T + a2 @ w2^T) + bias + rowbias[m // rows_per_group] + resid."""
+         out_dtype=BF16, accumulate=False, tail_group_n=0):
+    """out[M,N] = alpha*(a @ w^T + a2 @ w2^T) + bias + rowbias[m // rows_per_group] + resid.
+    tail_group_n > 0: output column group j uses a2[:, j*K2:(j+1)*K2] with w2 [N, K2]."""
     require_cuda(a, w)
     M, K1 = a.shape
     N = w.shape[0]
     assert w.shape[1] == K1 and a.dtype == BF16 and w.dtype == BF16
     K2 = 0
     if a2 is not None:
-        K2 = a2.shape[1]
-        assert w2.shape == (N, K2) and a2.shape[0] == M
+        K2 = w2.shape[1]
+        assert w2.shape[0] == N and a2.shape[0] == M
+        assert a2.shape[1] == (K2 * (N // tail_group_n) if tail_group_n else K2)
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=out_dtype)
     check(lib().pso_gemm(M, N, ptr(a), _row_stride(a), K1, ptr(w), _row_stride(w),
@@ -36,7 +38,8 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
                          ptr(w2), _row_stride(w2) if w2 is not None else 0,
                          float(alpha), ptr(bias), ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
                          int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
-                         ptr(out), _row_stride(out), dtype_code(out), int(accumulate), stream_ptr()), "pso_gemm")
+                         ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
+                         stream_ptr()), "pso_gemm")
     return out
 
 
@@ -248,11 +251,13 @@ def timestep_embedding(t, dim, out=None, out_col=0):
     return out
 
 
-def transpose(x, out=None):
+def transpose(x, out=None, pad_rows_to=1):
+    """[R, C] -> [C, Rp], Rp = R rounded up to pad_rows_to (pad columns are zero)."""
     R, C = x.shape
+    Rp = -(-R // pad_rows_to) * pad_rows_to
     if out is None:
-        out = torch.empty((C, R), device=x.device, dtype=x.dtype)
-    check(lib().pso_transpose(R, C, ptr(x), _row_stride(x), ptr(out), _row_stride(out), stream_ptr()),
+        out = torch.empty((C, Rp), device=x.device, dtype=x.dtype)
+    check(lib().pso_transpose(R, Rp, C, ptr(x), _row_stride(x), ptr(out), _row_stride(out), stream_ptr()),
           "pso_transpose")
     return out
 
@@ -302,4 +307,44 @@ def conv_weight_t(w, flip):
     out = torch.empty((Ci, ks, ks, Co), device=w.device, dtype=w.dtype)
     check(lib().pso_conv_weight_t(Co, ks, Ci, int(flip), ptr(w.contiguous()), ptr(out), stream_ptr()),
           "pso_conv_weight_t")
+    return out
+
+
+def concat_channels(x1, x2):
+    """[..., C1] ++ [..., C2] -> [..., C1+C2] (contiguous channels-last)."""
+    C1, C2 = x1.shape[-1], x2.shape[-1]
+    out = torch.empty(x1.shape[:-1] + (C1 + C2,), device=x1.device, dtype=x1.dtype)
+    npix = x1.numel() // C1
+    check(lib().pso_concat_channels(npix, C1, ptr(x1.contiguous()), C2, ptr(x2.contiguous()), ptr(out),
+                                    stream_ptr()), "pso_concat_channels")
+    return out
+
+
+def split_channels(x, C1, add2=None):
+    """inverse of concat_channels; the second part gets `add2` added when given."""
+    C = x.shape[-1]
+    C2 = C - C1
+    y1 = torch.empty(x.shape[:-1] + (C1,), device=x.device, dtype=x.dtype)
+    y2 = torch.empty(x.shape[:-1] + (C2,), device=x.device, dtype=x.dtype)
+    npix = x.numel() // C
+    check(lib().pso_split_channels(npix, C1, C2, ptr(x.contiguous()), ptr(y1), ptr(y2),
+                                   ptr(add2.contiguous()) if add2 is not None else None, stream_ptr()),
+          "pso_split_channels")
+    return y1, y2
+
+
+def nchw_to_nhwc(x):
+    """[B,C,H,W] fp32|bf16 -> [B,H,W,C] bf16."""
+    B, C, H, W = x.shape
+    out = torch.empty((B, H, W, C), device=x.device, dtype=BF16)
+    check(lib().pso_nchw_to_nhwc(B, C, H * W, ptr(x.contiguous()), dtype_code(x), ptr(out), stream_ptr()),
+          "pso_nchw_to_nhwc")
+    return out
+
+
+def nhwc_to_nchw(x, dtype=torch.float32):
+    B, H, W, C = x.shape
+    out = torch.empty((B, C, H, W), device=x.device, dtype=dtype)
+    check(lib().pso_nhwc_to_nchw(B, C, H * W, ptr(x.contiguous()), ptr(out), dtype_code(out), stream_ptr()),
+          "pso_nhwc_to_nchw")
     return out

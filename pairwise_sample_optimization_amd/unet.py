@@ -1,0 +1,894 @@
+"""SDXL UNet2DConditionModel (+ peft-style LoRA) on the libpso_amd HIP kernels, forward AND hand-written backward.
+
+Drop-in surface: `unet(sample, timestep, encoder_hidden_states, added_cond_kwargs={"time_ids",
+"text_embeds"}, return_dict=True)` -> object with `.sample` (or a tuple); `.config.in_channels`; `add_adapter(cfg)`;
+`disable_adapters()` / `enable_adapters()`; `enable_gradient_checkpointing()` (accepted, not needed: 288 GB HBM);
+`parameters()`; `load_state_dict()` / `state_dict()` in diffusers key layout; `from_config(...)`.
+Architecture restated from diffusers 0.27.0 (environment.yml:15; called at T:775-805, D:777-806,
+DP/sdxl_turbo_with_logprob.py:126-132): conv_in -> 3 down blocks (320/640/1280; transformer depth 0/2/10) -> mid
+(depth 10) -> 3 up blocks -> GroupNorm+SiLU -> conv_out; Timesteps(320)->MLP time embedding + the SDXL "text_time"
+added embedding; BasicTransformerBlock = LN/self-attn/LN/cross-attn(77x2048)/LN/GEGLU FF; LoRA (rank r, alpha r) on
+to_q/to_k/to_v/to_out.0 of all attentions (T:338-345).
+
+MI355X-first design:
+  * activations channels-last bf16 ([tokens, C] / NHWC), fp32 statistics and accumulation;
+  * each diffusers Linear/Conv is one MFMA GEMM launch with bias / time-embedding / residual fused in the epilogue;
+    self-attention q/k/v is ONE fused projection whose three LoRA up-projections are fused as a grouped K-tail;
+  * the whole UNet is ONE autograd node: forward keeps exactly the tensors its hand-written backward needs (no
+    gradient checkpoint recompute -- the reference's T:358 trades 6.8 TFLOP/img for memory that 288 GB HBM has);
+  * LoRA masters are one flat fp32 buffer and their gradients one flat fp32 buffer that the backward GEMMs
+    accumulate into directly (f32-accumulate epilogue) -- the all-reduce bucket and the optimizer operand.
+"""
+import math
+from dataclasses import dataclass, field, replace
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+
+
+# ======================================================================================================================
+# config
+# ======================================================================================================================
+@dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: tuple = (320, 640, 1280)
+    layers_per_block: int = 2
+    transformer_layers_per_block: tuple = (1, 2, 10)
+    down_has_attn: tuple = (False, True, True)
+    head_dim: int = 64
+    cross_attention_dim: int = 2048
+    addition_time_embed_dim: int = 256
+    text_embed_dim: int = 1280
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-5
+    time_proj_dim: int = 320
+    sample_size: int = 128
+
+    @property
+    def time_embed_dim(self):
+        return 4 * self.block_out_channels[0]
+
+    @property
+    def projection_class_embeddings_input_dim(self):
+        return self.text_embed_dim + 6 * self.addition_time_embed_dim
+
+    @staticmethod
+    def sdxl(sample_size=128):
+        return UNetConfig(sample_size=sample_size)
+
+    @staticmethod
+    def tiny(sample_size=16):
+        """Same topology, small widths (parity tests)."""
+        return UNetConfig(block_out_channels=(64, 128, 128), transformer_layers_per_block=(1, 1, 2),
+                          cross_attention_dim=128, addition_time_embed_dim=32, text_embed_dim=64, time_proj_dim=64,
+                          sample_size=sample_size)
+
+
+# ======================================================================================================================
+# parameter holders (diffusers names / layouts) + kernel-layout caches
+# ======================================================================================================================
+def _param(*shape):
+    return nn.Parameter(torch.empty(*shape, dtype=BF16), requires_grad=False)
+
+
+class Linear(nn.Module):
+    def __init__(self, fin, fout, bias=True):
+        super().__init__()
+        self.in_features, self.out_features = fin, fout
+        self.weight = _param(fout, fin)
+        self.bias = _param(fout) if bias else None
+
+    def reset(self, g):
+        bound = 1.0 / math.sqrt(self.in_features)
+        with torch.no_grad():
+            self.weight.copy_((torch.rand(self.weight.shape, generator=g) * 2 - 1) * bound)
+            if self.bias is not None:
+                self.bias.copy_((torch.rand(self.bias.shape, generator=g) * 2 - 1) * bound)
+
+    def prepare(self):
+        self.wt = K.transpose(self.weight.data)  # [in][out] for the input gradient
+
+
+class Conv2d(nn.Module):
+    def __init__(self, cin, cout, k, stride=1, bias=True):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.weight = _param(cout, cin, k, k)
+        self.bias = _param(cout) if bias else None
+
+    def reset(self, g):
+        bound = 1.0 / math.sqrt(self.cin * self.k * self.k)
+        with torch.no_grad():
+            self.weight.copy_((torch.rand(self.weight.shape, generator=g) * 2 - 1) * bound)
+            if self.bias is not None:
+                self.bias.copy_((torch.rand(self.bias.shape, generator=g) * 2 - 1) * bound)
+
+    def prepare(self):
+        w = self.weight.data
+        self.w_nhwc = w.permute(0, 2, 3, 1).contiguous()  # [Co][kh][kw][Ci]  (one-time layout change at load)
+        if self.k == 1:
+            self.w_mat = self.w_nhwc.view(self.cout, self.cin)
+            self.wt = K.transpose(self.w_mat)
+        elif self.cin % 64 != 0:  # conv_in: im2col GEMM, K = 9*Ci padded to 64
+            kp = 64 * ((9 * self.cin + 63) // 64)
+            self.kp = kp
+            self.w_col = torch.zeros(self.cout, kp, device=w.device, dtype=BF16)
+            self.w_col[:, :9 * self.cin] = self.w_nhwc.reshape(self.cout, -1)
+        else:
+            # input-gradient weights: stride 1 -> rotated taps; stride 2 -> unrotated taps (T2 gather)
+            self.w_dx = K.conv_weight_t(self.w_nhwc, flip=(self.stride == 1))
+            if self.cout % 64 != 0:  # conv_out (Co=4): the input-gradient conv has C=4 -> im2col GEMM
+                kp = 64 * ((9 * self.cout + 63) // 64)
+                self.kp_dx = kp
+                self.w_dx_col = torch.zeros(self.cin, kp, device=w.device, dtype=BF16)
+                self.w_dx_col[:, :9 * self.cout] = self.w_dx.reshape(self.cin, -1)
+
+
+class Norm(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.weight = _param(c)
+        self.bias = _param(c)
+
+    def reset(self, g):
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+            self.bias.zero_()
+
+
+# ======================================================================================================================
+# LoRA state: flat fp32 masters + flat fp32 grads (the all-reduce bucket), bf16 working copies
+# ======================================================================================================================
+class LoraState:
+    """peft LoraConfig(r, lora_alpha=r, init_lora_weights="gaussian", target_modules=[to_k,to_q,to_v,to_out.0])
+    (T:338-345): A ~ N(0, 1/r) [r, in], B = 0 [out, r], scaling alpha/r.  Entries are laid out in reverse forward
+    order, i.e. the order the backward produces their gradients (for bucketed all-reduce)."""
+
+    def __init__(self, entries, r, alpha, device):
+        self.r, self.alpha, self.scale = r, alpha, alpha / r
+        self.entries = entries  # list of (name, fin, fout) in forward order
+        self.index = {}
+        off = 0
+        for name, fin, fout in reversed(entries):
+            self.index[name] = (off, fin, fout)
+            off += r * fin + fout * r
+        self.numel = off
+        self.master = torch.zeros(off, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(off, device=device, dtype=torch.float32)
+        self.work = torch.zeros(off, device=device, dtype=BF16)  # bf16 copy (B pre-scaled)
+        self.param = nn.Parameter(self.master, requires_grad=True)  # autograd trigger for the UNet node
+        self.cache = {}
+
+    def views(self, t, name):
+        off, fin, fout = self.index[name]
+        r = self.r
+        return t[off:off + r * fin].view(r, fin), t[off + r * fin:off + r * fin + fout * r].view(fout, r)
+
+    def init_gaussian(self, seed=0, b_std=0.0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        for name, fin, fout in self.entries:
+            A, B = self.views(self.master, name)
+            A.copy_(torch.randn(A.shape, generator=g) / self.r)  # peft gaussian: std 1/r
+            if b_std:
+                B.copy_(torch.randn(B.shape, generator=g) * b_std)
+            else:
+                B.zero_()
+        self.refresh()
+
+    def refresh(self):
+        """bf16 working copies and transposed forms after a master update (one cast + per-adapter transposes)."""
+        K.cast_f32_bf16(self.master, out=self.work)
+        if self.scale != 1.0:
+            for name in self.index:
+                _, Bw = self.views(self.work, name)
+                K.axpby(self.scale, Bw.contiguous(), out=Bw)
+        self.cache = {}
+        for name in self.index:
+            A, B = self.views(self.work, name)
+            self.cache[name] = SimpleNamespace(A=A, sB=B, At=K.transpose(A), sBt=K.transpose(B))
+
+    def grad_views(self, name):
+        return self.views(self.grad, name)
+
+    def state_dict_peft(self):
+        """{module_path.lora_A.weight, module_path.lora_B.weight} (get_peft_model_state_dict naming)."""
+        out = {}
+        for name in self.index:
+            A, B = self.views(self.master, name)
+            out[f"{name}.lora_A.weight"] = A.detach().clone()
+            out[f"{name}.lora_B.weight"] = B.detach().clone()
+        return out
+
+    def load_peft(self, sd):
+        for name in self.index:
+            A, B = self.views(self.master, name)
+            A.copy_(sd[f"{name}.lora_A.weight"])
+            B.copy_(sd[f"{name}.lora_B.weight"])
+        self.refresh()
+
+
+def _T(x, pad_to=8):
+    """[M][C] -> [C][Mp] with the reduction dim zero-padded to a multiple of `pad_to` (GEMM K % 8 == 0)."""
+    return K.transpose(x, pad_rows_to=pad_to)
+
+
+def _lora_dw(st, name, v, x, dy, u):
+    """LoRA parameter gradients, accumulated into the flat fp32 grad buffer:
+    dA[r][in] += v^T x ,  dB[out][r] += s * dy^T u   (v = dy (sB), u = x A^T)."""
+    gA, gB = st.grad_views(name)
+    K.gemm(_T(v), _T(x), out=gA, out_dtype=torch.float32, accumulate=True)
+    K.gemm(_T(dy), _T(u), out=gB, out_dtype=torch.float32, accumulate=True, alpha=st.scale)
+
+
+# ======================================================================================================================
+# blocks: fwd(x, rt) -> y (saving what bwd needs in a dict when rt.save) ; bwd(dy, saved, rt) -> dx
+# ======================================================================================================================
+class Attention(nn.Module):
+    """diffusers Attention (heads = dim/64, to_q/to_k/to_v without bias, to_out.0 with bias)."""
+
+    def __init__(self, dim, kv_dim):
+        super().__init__()
+        self.dim, self.kv_dim, self.heads = dim, kv_dim, dim // 64
+        self.to_q = Linear(dim, dim, bias=False)
+        self.to_k = Linear(kv_dim, dim, bias=False)
+        self.to_v = Linear(kv_dim, dim, bias=False)
+        self.to_out = nn.ModuleList([Linear(dim, dim)])
+
+    def prepare(self, self_attn):
+        C = self.dim
+        if self_attn:
+            self.w_qkv = torch.cat([self.to_q.weight.data, self.to_k.weight.data, self.to_v.weight.data], 0)
+            self.wt_qkv = K.transpose(self.w_qkv)  # [C][3C]
+        else:
+            self.w_kv = torch.cat([self.to_k.weight.data, self.to_v.weight.data], 0)
+            self.to_q.prepare()
+        self.to_out[0].prepare()
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, cross_dim):
+        super().__init__()
+        self.dim = dim
+        self.norm1, self.norm2, self.norm3 = Norm(dim), Norm(dim), Norm(dim)
+        self.attn1 = Attention(dim, dim)
+        self.attn2 = Attention(dim, cross_dim)
+        self.ff = SimpleFF(dim)
+
+    def prepare(self):
+        self.attn1.prepare(True)
+        self.attn2.prepare(False)
+        self.ff.prepare()
+
+    def lora_entries(self, path):
+        e = []
+        for an, a in (("attn1", self.attn1), ("attn2", self.attn2)):
+            for tn, fin in (("to_q", a.dim), ("to_k", a.kv_dim), ("to_v", a.kv_dim), ("to_out.0", a.dim)):
+                e.append((f"{path}.{an}.{tn}", fin, a.dim))
+        return e
+
+    def fwd(self, x, rt, path):
+        """x [M, C] (M = B*S).  Returns h3 [M, C]."""
+        C, M, B = self.dim, x.shape[0], rt.B
+        S = M // B
+        a1m, a2m = self.attn1, self.attn2
+        lo = rt.lora_on
+        L = (lambda n: rt.lora.cache[f"{path}.{n}"]) if lo else None
+        sv = {} if rt.save else None
+        # --- self attention ---
+        n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
+        if lo:
+            lq, lk, lv = L("attn1.to_q"), L("attn1.to_k"), L("attn1.to_v")
+            u_qkv = torch.empty((M, 3 * rt.r), device=x.device, dtype=BF16)
+            for j, l in enumerate((lq, lk, lv)):
+                K.gemm(n1, l.A, out=u_qkv[:, j * rt.r:(j + 1) * rt.r])
+            sB = rt.lora_qkv_sB[path]
+            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=sB, tail_group_n=C)
+        else:
+            qkv = K.gemm(n1, a1m.w_qkv)
+        q3 = qkv.view(B, S, 3 * C)
+        a1, lse1 = K.attention_fwd(q3[..., :C], q3[..., C:2 * C], q3[..., 2 * C:], a1m.heads)
+        a1 = a1.view(M, C)
+        o1 = a1m.to_out[0]
+        if lo:
+            lo1 = L("attn1.to_out.0")
+            u_o1 = K.gemm(a1, lo1.A)
+            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=lo1.sB)
+        else:
+            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x)
+        # --- cross attention ---
+        n2, st2 = K.layer_norm_fwd(h1, self.norm2.weight, self.norm2.bias, 1e-5)
+        enc = rt.enc  # [B*77, Dc]
+        Se = enc.shape[0] // B
+        if lo:
+            lq2, lk2, lv2 = L("attn2.to_q"), L("attn2.to_k"), L("attn2.to_v")
+            u_q2 = K.gemm(n2, lq2.A)
+            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=lq2.sB)
+            u_kv2 = torch.empty((enc.shape[0], 2 * rt.r), device=x.device, dtype=BF16)
+            K.gemm(enc, lk2.A, out=u_kv2[:, :rt.r])
+            K.gemm(enc, lv2.A, out=u_kv2[:, rt.r:])
+            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=rt.lora_kv_sB[path], tail_group_n=C)
+        else:
+            q2 = K.gemm(n2, a2m.to_q.weight)
+            kv2 = K.gemm(enc, a2m.w_kv)
+        kv3 = kv2.view(B, Se, 2 * C)
+        a2, lse2 = K.attention_fwd(q2.view(B, S, C), kv3[..., :C], kv3[..., C:], a2m.heads)
+        a2 = a2.view(M, C)
+        o2 = a2m.to_out[0]
+        if lo:
+            lo2 = L("attn2.to_out.0")
+            u_o2 = K.gemm(a2, lo2.A)
+            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=lo2.sB)
+        else:
+            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
+        # --- GEGLU feed-forward ---
+        n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
+        f = K.gemm(n3, self.ff.proj.weight, bias=self.ff.proj.bias)
+        gg = K.geglu_fwd(f)
+        h3 = K.gemm(gg, self.ff.out.weight, bias=self.ff.out.bias, resid=h2)
+        if sv is not None:
+            sv.update(x=x, st1=st1, n1=n1, qkv=qkv, a1=a1, lse1=lse1, h1=h1, st2=st2, n2=n2, q2=q2, kv2=kv2, a2=a2,
+                      lse2=lse2, h2=h2, st3=st3, f=f)
+            if lo:
+                sv.update(u_qkv=u_qkv, u_o1=u_o1, u_q2=u_q2, u_kv2=u_kv2, u_o2=u_o2)
+            rt.saved.append(sv)
+        return h3
+
+    def bwd(self, dh3, sv, rt, path):
+        C = self.dim
+        B = rt.B
+        M = dh3.shape[0]
+        S = M // B
+        r = rt.r
+        lo = rt.lora_on
+        st = rt.lora
+        L = (lambda n: st.cache[f"{path}.{n}"]) if lo else None
+        a1m, a2m = self.attn1, self.attn2
+        # --- FF ---
+        dg = K.gemm(dh3, self.ff.out.wt)
+        df = K.geglu_bwd(sv["f"], dg)
+        dn3 = K.gemm(df, self.ff.proj.wt)
+        dh2 = K.layer_norm_bwd(sv["h2"], dn3, sv["st3"], self.norm3.weight, dadd=dh3)
+        # --- cross attention out-proj ---
+        o2 = a2m.to_out[0]
+        if lo:
+            lo2 = L("attn2.to_out.0")
+            v_o2 = K.gemm(dh2, lo2.sBt)
+            da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=lo2.At)
+            _lora_dw(st, f"{path}.attn2.to_out.0", v_o2, sv["a2"], dh2, sv["u_o2"])
+        else:
+            da2 = K.gemm(dh2, o2.wt)
+        enc = rt.enc
+        Se = enc.shape[0] // B
+        kv3 = sv["kv2"].view(B, Se, 2 * C)
+        dkv2 = torch.empty((B * Se, 2 * C), device=dh3.device, dtype=BF16)
+        dk3 = dkv2.view(B, Se, 2 * C)
+        dq2, _, _ = K.attention_bwd(sv["q2"].view(B, S, C), kv3[..., :C], kv3[..., C:], sv["a2"].view(B, S, C),
+                                    sv["lse2"], da2.view(B, S, C), a2m.heads, dk=dk3[..., :C], dv=dk3[..., C:])
+        dq2 = dq2.view(M, C)
+        if lo:
+            lq2, lk2, lv2 = L("attn2.to_q"), L("attn2.to_k"), L("attn2.to_v")
+            v_q2 = K.gemm(dq2, lq2.sBt)
+            dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=lq2.At)
+            _lora_dw(st, f"{path}.attn2.to_q", v_q2, sv["n2"], dq2, sv["u_q2"])
+            dk2, dv2 = dkv2[:, :C], dkv2[:, C:]
+            u_kv2 = sv["u_kv2"]
+            for nm, l, dd, uu in (("to_k", lk2, dk2, u_kv2[:, :r]), ("to_v", lv2, dv2, u_kv2[:, r:])):
+                vv = K.gemm(dd, l.sBt)
+                gA, gB = st.grad_views(f"{path}.attn2.{nm}")
+                K.gemm(_T(vv), rt.enc_t, out=gA, out_dtype=torch.float32, accumulate=True)
+                K.gemm(_T(dd), _T(uu), out=gB, out_dtype=torch.float32, accumulate=True, alpha=st.scale)
+        else:
+            dn2 = K.gemm(dq2, a2m.to_q.wt)
+        dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
+        # --- self attention ---
+        o1 = a1m.to_out[0]
+        if lo:
+            lo1 = L("attn1.to_out.0")
+            v_o1 = K.gemm(dh1, lo1.sBt)
+            da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=lo1.At)
+            _lora_dw(st, f"{path}.attn1.to_out.0", v_o1, sv["a1"], dh1, sv["u_o1"])
+        else:
+            da1 = K.gemm(dh1, o1.wt)
+        q3 = sv["qkv"].view(B, S, 3 * C)
+        dqkv = torch.empty((M, 3 * C), device=dh3.device, dtype=BF16)
+        d3 = dqkv.view(B, S, 3 * C)
+        K.attention_bwd(q3[..., :C], q3[..., C:2 * C], q3[..., 2 * C:], sv["a1"].view(B, S, C), sv["lse1"],
+                        da1.view(B, S, C), a1m.heads, dq=d3[..., :C], dk=d3[..., C:2 * C], dv=d3[..., 2 * C:])
+        if lo:
+            v_qkv = torch.empty((M, 3 * r), device=dh3.device, dtype=BF16)
+            names = ("to_q", "to_k", "to_v")
+            for j, nm in enumerate(names):
+                K.gemm(dqkv[:, j * C:(j + 1) * C], L(f"attn1.{nm}").sBt, out=v_qkv[:, j * r:(j + 1) * r])
+            dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=rt.lora_qkv_At[path])
+            n1t = _T(sv["n1"])
+            vt = _T(v_qkv)
+            ut = _T(sv["u_qkv"])
+            for j, nm in enumerate(names):
+                gA, gB = st.grad_views(f"{path}.attn1.{nm}")
+                K.gemm(vt[j * r:(j + 1) * r], n1t, out=gA, out_dtype=torch.float32, accumulate=True)
+                K.gemm(_T(dqkv[:, j * C:(j + 1) * C]), ut[j * r:(j + 1) * r], out=gB, out_dtype=torch.float32,
+                       accumulate=True, alpha=st.scale)
+        else:
+            dn1 = K.gemm(dqkv, a1m.wt_qkv)
+        return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
+
+
+class SimpleFF(nn.Module):
+    """diffusers FeedForward(dim, activation_fn="geglu"): net.0 = GEGLU(proj: dim -> 8*dim), net.2 = Linear(4dim->dim)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.proj = Linear(dim, 8 * dim)
+        self.out = Linear(4 * dim, dim)
+
+    def prepare(self):
+        self.proj.prepare()
+        self.out.prepare()
+
+    def _remap(self):
+        return {"net.0.proj": self.proj, "net.2": self.out}
+
+
+class Transformer2DModel(nn.Module):
+    """use_linear_projection=True: GN(eps 1e-6) -> proj_in -> blocks -> proj_out + residual."""
+
+    def __init__(self, C, depth, cross_dim, groups):
+        super().__init__()
+        self.C, self.groups = C, groups
+        self.norm = Norm(C)
+        self.proj_in = Linear(C, C)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(C, cross_dim) for _ in range(depth)])
+        self.proj_out = Linear(C, C)
+
+    def prepare(self):
+        self.proj_in.prepare()
+        self.proj_out.prepare()
+        for b in self.transformer_blocks:
+            b.prepare()
+
+    def fwd(self, x, rt, path):
+        """x NHWC [B,H,W,C] -> same shape."""
+        B, H, W, C = x.shape
+        xn, st = K.group_norm_fwd(x, self.norm.weight, self.norm.bias, self.groups, 1e-6, False)
+        h = K.gemm(xn.view(-1, C), self.proj_in.weight, bias=self.proj_in.bias)
+        if rt.save:
+            rt.saved.append({"x": x, "st": st})
+        for i, blk in enumerate(self.transformer_blocks):
+            h = blk.fwd(h, rt, f"{path}.transformer_blocks.{i}")
+        return K.gemm(h, self.proj_out.weight, bias=self.proj_out.bias, resid=x.view(-1, C)).view(B, H, W, C)
+
+    def bwd(self, dy, rt, path):
+        B, H, W, C = dy.shape
+        d2 = dy.view(-1, C)
+        dh = K.gemm(d2, self.proj_out.wt)
+        for i in reversed(range(len(self.transformer_blocks))):
+            dh = self.transformer_blocks[i].bwd(dh, rt.saved.pop(), rt, f"{path}.transformer_blocks.{i}")
+        sv = rt.saved.pop()
+        dn = K.gemm(dh, self.proj_in.wt).view(B, H, W, C)
+        return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin, cout, groups, eps, temb_dim):
+        super().__init__()
+        self.cin, self.cout, self.groups, self.eps = cin, cout, groups, eps
+        self.norm1 = Norm(cin)
+        self.conv1 = Conv2d(cin, cout, 3)
+        self.time_emb_proj = Linear(temb_dim, cout) if temb_dim else None
+        self.norm2 = Norm(cout)
+        self.conv2 = Conv2d(cout, cout, 3)
+        self.conv_shortcut = Conv2d(cin, cout, 1) if cin != cout else None
+
+    def prepare(self):
+        self.conv1.prepare()
+        self.conv2.prepare()
+        if self.conv_shortcut is not None:
+            self.conv_shortcut.prepare()
+
+    def fwd(self, x, rt, temb=None):
+        """x NHWC [B,H,W,Ci]; temb [B, Co] row view (time_emb_proj output) or None."""
+        h1, st1 = K.group_norm_fwd(x, self.norm1.weight, self.norm1.bias, self.groups, self.eps, True)
+        c1 = K.conv2d(h1, self.conv1.w_nhwc, bias=self.conv1.bias, rowbias=temb)
+        h2, st2 = K.group_norm_fwd(c1, self.norm2.weight, self.norm2.bias, self.groups, self.eps, True)
+        if self.conv_shortcut is not None:
+            B, H, W, _ = x.shape
+            sc = K.gemm(x.view(-1, self.cin), self.conv_shortcut.w_mat, bias=self.conv_shortcut.bias)
+            sc = sc.view(B, H, W, self.cout)
+        else:
+            sc = x
+        out = K.conv2d(h2, self.conv2.w_nhwc, bias=self.conv2.bias, resid=sc)
+        if rt.save:
+            rt.saved.append({"x": x, "st1": st1, "c1": c1, "st2": st2})
+        return out
+
+    def bwd(self, dout, rt):
+        sv = rt.saved.pop()
+        dh2 = K.conv2d(dout, self.conv2.w_dx)
+        dc1 = K.group_norm_bwd(sv["c1"], dh2, sv["st2"], self.norm2.weight, self.norm2.bias, True)
+        dh1 = K.conv2d(dc1, self.conv1.w_dx)
+        if self.conv_shortcut is not None:
+            B, H, W, _ = dout.shape
+            dsc = K.gemm(dout.view(-1, self.cout), self.conv_shortcut.wt).view(B, H, W, self.cin)
+        else:
+            dsc = dout
+        return K.group_norm_bwd(sv["x"], dh1, sv["st1"], self.norm1.weight, self.norm1.bias, True, dadd=dsc)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.conv = Conv2d(C, C, 3, stride=2)
+
+    def prepare(self):
+        self.conv.prepare()
+
+    def fwd(self, x, rt):
+        if rt.save:
+            rt.saved.append({"hw": x.shape[1:3]})
+        return K.conv2d(x, self.conv.w_nhwc, stride=2, bias=self.conv.bias)
+
+    def bwd(self, dy, rt):
+        sv = rt.saved.pop()
+        return K.conv2d(dy, self.conv.w_dx, mode=K.CONV_T2, out_hw=tuple(sv["hw"]))
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, C):
+        super().__init__()
+        self.conv = Conv2d(C, C, 3)
+
+    def prepare(self):
+        self.conv.prepare()
+
+    def fwd(self, x, rt):
+        return K.conv2d(x, self.conv.w_nhwc, mode=K.CONV_UP2, bias=self.conv.bias)
+
+    def bwd(self, dy, rt):
+        du = K.conv2d(dy, self.conv.w_dx)  # input-gradient on the 2x grid
+        return K.sumpool2(du)
+
+
+class _Block(nn.Module):
+    """down / up / mid block container with diffusers child names."""
+
+    def __init__(self):
+        super().__init__()
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, fin, dim):
+        super().__init__()
+        self.linear_1 = Linear(fin, dim)
+        self.linear_2 = Linear(dim, dim)
+
+
+# ======================================================================================================================
+# the model
+# ======================================================================================================================
+class _Output(SimpleNamespace):
+    pass
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, config: UNetConfig = None):
+        super().__init__()
+        cfg = config or UNetConfig.sdxl()
+        self.cfg = cfg
+        self.config = SimpleNamespace(in_channels=cfg.in_channels, out_channels=cfg.out_channels,
+                                      sample_size=cfg.sample_size, block_out_channels=cfg.block_out_channels,
+                                      cross_attention_dim=cfg.cross_attention_dim)
+        ch = cfg.block_out_channels
+        G, eps, tdim = cfg.norm_num_groups, cfg.norm_eps, cfg.time_embed_dim
+        self.conv_in = Conv2d(cfg.in_channels, ch[0], 3)
+        self.time_embedding = TimestepEmbedding(cfg.time_proj_dim, tdim)
+        self.add_embedding = TimestepEmbedding(cfg.projection_class_embeddings_input_dim, tdim)
+        nlev = len(ch)
+        self.down_blocks = nn.ModuleList()
+        cin = ch[0]
+        for i in range(nlev):
+            blk = _Block()
+            blk.resnets = nn.ModuleList()
+            if cfg.down_has_attn[i]:
+                blk.attentions = nn.ModuleList()
+            for j in range(cfg.layers_per_block):
+                blk.resnets.append(ResnetBlock2D(cin if j == 0 else ch[i], ch[i], G, eps, tdim))
+                if cfg.down_has_attn[i]:
+                    blk.attentions.append(Transformer2DModel(ch[i], cfg.transformer_layers_per_block[i],
+                                                             cfg.cross_attention_dim, G))
+            if i < nlev - 1:
+                blk.downsamplers = nn.ModuleList([Downsample2D(ch[i])])
+            cin = ch[i]
+            self.down_blocks.append(blk)
+        mid = _Block()
+        mid.resnets = nn.ModuleList([ResnetBlock2D(ch[-1], ch[-1], G, eps, tdim),
+                                     ResnetBlock2D(ch[-1], ch[-1], G, eps, tdim)])
+        mid.attentions = nn.ModuleList([Transformer2DModel(ch[-1], cfg.transformer_layers_per_block[-1],
+                                                           cfg.cross_attention_dim, G)])
+        self.mid_block = mid
+        self.up_blocks = nn.ModuleList()
+        rch = list(reversed(ch))
+        rattn = list(reversed(cfg.down_has_attn))
+        rdepth = list(reversed(cfg.transformer_layers_per_block))
+        prev = ch[-1]
+        for i in range(nlev):
+            out_c = rch[i]
+            in_c = rch[min(i + 1, nlev - 1)]
+            blk = _Block()
+            blk.resnets = nn.ModuleList()
+            if rattn[i]:
+                blk.attentions = nn.ModuleList()
+            n = cfg.layers_per_block + 1
+            for j in range(n):
+                skip_c = in_c if j == n - 1 else out_c
+                res_in = prev if j == 0 else out_c
+                blk.resnets.append(ResnetBlock2D(res_in + skip_c, out_c, G, eps, tdim))
+                if rattn[i]:
+                    blk.attentions.append(Transformer2DModel(out_c, rdepth[i], cfg.cross_attention_dim, G))
+            if i < nlev - 1:
+                blk.upsamplers = nn.ModuleList([Upsample2D(out_c)])
+            prev = out_c
+            self.up_blocks.append(blk)
+        self.conv_norm_out = Norm(ch[0])
+        self.conv_out = Conv2d(ch[0], cfg.out_channels, 3)
+        self.lora = None
+        self._adapters_enabled = True
+        self._prepared = False
+        self.gradient_checkpointing = False
+
+    # ---------------- parameter plumbing ----------------
+    def _remap_key(self, k):
+        return k.replace(".ff.net.0.proj.", ".ff.proj.").replace(".ff.net.2.", ".ff.out.")
+
+    def _unmap_key(self, k):
+        return k.replace(".ff.proj.", ".ff.net.0.proj.").replace(".ff.out.", ".ff.net.2.")
+
+    def state_dict(self, *a, **kw):
+        sd = super().state_dict(*a, **kw)
+        return {self._unmap_key(k): v for k, v in sd.items()}
+
+    def load_state_dict(self, sd, strict=True):
+        sd = {self._remap_key(k): v for k, v in sd.items()}
+        res = super().load_state_dict({k: v.to(BF16) for k, v in sd.items()}, strict=strict)
+        self._prepared = False
+        return res
+
+    @classmethod
+    def from_config(cls, config=None, **kw):
+        return cls(config if isinstance(config, UNetConfig) else UNetConfig.sdxl())
+
+    def init_weights(self, seed=0):
+        """PyTorch-default-style seeded init (the BASELINE synthetic-weights recipe); norms at identity."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        for m in self.modules():
+            if isinstance(m, (Linear, Conv2d, Norm)):
+                m.reset(g)
+        self._prepared = False
+        return self
+
+    def enable_gradient_checkpointing(self):
+        self.gradient_checkpointing = True  # accepted for API parity; activations are kept (288 GB HBM)
+
+    def _attn_modules(self):
+        for name, m in self.named_modules():
+            if isinstance(m, BasicTransformerBlock):
+                yield name, m
+
+    def add_adapter(self, lora_config):
+        """peft LoraConfig(r, lora_alpha, init_lora_weights='gaussian', target_modules=[to_k,to_q,to_v,to_out.0])."""
+        r = getattr(lora_config, "r", 32)
+        alpha = getattr(lora_config, "lora_alpha", r)
+        entries = []
+        for name, blk in self._attn_modules():
+            entries += blk.lora_entries(name)
+        dev = self.conv_in.weight.device
+        self.lora = LoraState(entries, r, alpha, dev)
+        if dev.type == "cuda":
+            self.lora.init_gaussian(seed=getattr(lora_config, "seed", 0))
+        self._adapters_enabled = True
+        return self.lora
+
+    def disable_adapters(self):
+        self._adapters_enabled = False
+
+    def enable_adapters(self):
+        self._adapters_enabled = True
+
+    def lora_parameters(self):
+        return [self.lora.param] if self.lora is not None else []
+
+    def prepare(self):
+        """Derive kernel-layout weight caches (one-time after load; weights are frozen in LoRA training)."""
+        for m in self.modules():
+            if isinstance(m, (Transformer2DModel, ResnetBlock2D, Downsample2D, Upsample2D)):
+                m.prepare()
+        # the time-embedding projections of all resnets as ONE GEMM
+        res = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        self._temb_w = torch.cat([m.time_emb_proj.weight.data for m in res], 0)
+        self._temb_b = torch.cat([m.time_emb_proj.bias.data for m in res], 0)
+        off = 0
+        for m in res:
+            m._temb_off = off
+            off += m.cout
+        self._temb_n = off
+        self.conv_in.prepare()
+        self.conv_out.prepare()
+        self._prepared = True
+        if self.lora is not None:
+            self.refresh_lora()
+
+    def refresh_lora(self):
+        st = self.lora
+        st.refresh()
+        r = st.r
+        self._lora_qkv_sB, self._lora_qkv_At, self._lora_kv_sB = {}, {}, {}
+        for name, blk in self._attn_modules():
+            c = st.cache
+            q, k, v = (c[f"{name}.attn1.{t}"] for t in ("to_q", "to_k", "to_v"))
+            self._lora_qkv_sB[name] = torch.cat([q.sB, k.sB, v.sB], 0)       # [3C][r]
+            self._lora_qkv_At[name] = torch.cat([q.At, k.At, v.At], 1)       # [C][3r]
+            k2, v2 = c[f"{name}.attn2.to_k"], c[f"{name}.attn2.to_v"]
+            self._lora_kv_sB[name] = torch.cat([k2.sB, v2.sB], 0)            # [2C][r]
+
+    # ---------------- forward / backward ----------------
+    def _runtime(self, B, enc, save, lora_on):
+        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on)
+        if lora_on:
+            rt.lora = self.lora
+            rt.r = self.lora.r
+            rt.lora_qkv_sB, rt.lora_qkv_At, rt.lora_kv_sB = self._lora_qkv_sB, self._lora_qkv_At, self._lora_kv_sB
+        else:
+            rt.r = 0
+        return rt
+
+    def _embed(self, timestep, time_ids, text_embeds, B, dev):
+        cfg = self.cfg
+        t = torch.as_tensor(timestep, device=dev).float().reshape(-1)
+        if t.numel() == 1:
+            t = t.expand(B).contiguous()
+        te = K.timestep_embedding(t, cfg.time_proj_dim)
+        l1, l2 = self.time_embedding.linear_1, self.time_embedding.linear_2
+        emb = K.gemm(K.silu(K.gemm(te, l1.weight, bias=l1.bias)), l2.weight, bias=l2.bias)
+        tid = K.timestep_embedding(time_ids.reshape(-1), cfg.addition_time_embed_dim).view(B, -1)
+        add_in = K.concat_channels(text_embeds.to(BF16).contiguous(), tid)
+        a1, a2 = self.add_embedding.linear_1, self.add_embedding.linear_2
+        emb = K.gemm(K.silu(K.gemm(add_in, a1.weight, bias=a1.bias)), a2.weight, bias=a2.bias, resid=emb)
+        return K.gemm(K.silu(emb), self._temb_w, bias=self._temb_b)  # [B, sum Co]
+
+    def forward_nhwc(self, x, timestep, enc, text_embeds, time_ids, save=False):
+        """Core forward.  x NHWC bf16 [B,h,w,4]; enc [B,77,Dc]; returns eps NHWC bf16 [B,h,w,4]."""
+        if not self._prepared:
+            self.prepare()
+        B = x.shape[0]
+        lora_on = self.lora is not None and self._adapters_enabled
+        encf = enc.to(BF16).reshape(B * enc.shape[1], enc.shape[2]).contiguous()
+        rt = self._runtime(B, encf, save, lora_on)
+        if save and lora_on:
+            rt.enc_t = _T(encf)
+        temb_all = self._embed(timestep, time_ids, text_embeds, B, x.device)
+        tb = lambda m: temb_all[:, m._temb_off:m._temb_off + m.cout]
+        # conv_in (C=4): im2col GEMM
+        _, H, W, _ = x.shape
+        cols = K.im2col3(x, self.conv_in.kp)
+        h = K.gemm(cols, self.conv_in.w_col, bias=self.conv_in.bias).view(B, H, W, -1)
+        skips = [h]
+        for i, blk in enumerate(self.down_blocks):
+            for j, res in enumerate(blk.resnets):
+                h = res.fwd(h, rt, tb(res))
+                if hasattr(blk, "attentions"):
+                    h = blk.attentions[j].fwd(h, rt, f"down_blocks.{i}.attentions.{j}")
+                skips.append(h)
+            if hasattr(blk, "downsamplers"):
+                h = blk.downsamplers[0].fwd(h, rt)
+                skips.append(h)
+        m = self.mid_block
+        h = m.resnets[0].fwd(h, rt, tb(m.resnets[0]))
+        h = m.attentions[0].fwd(h, rt, "mid_block.attentions.0")
+        h = m.resnets[1].fwd(h, rt, tb(m.resnets[1]))
+        for i, blk in enumerate(self.up_blocks):
+            for j, res in enumerate(blk.resnets):
+                s = skips.pop()
+                hc = K.concat_channels(h, s)
+                if save:
+                    rt.saved.append({"c1": h.shape[-1]})
+                h = res.fwd(hc, rt, tb(res))
+                if hasattr(blk, "attentions"):
+                    h = blk.attentions[j].fwd(h, rt, f"up_blocks.{i}.attentions.{j}")
+            if hasattr(blk, "upsamplers"):
+                h = blk.upsamplers[0].fwd(h, rt)
+        hn, st = K.group_norm_fwd(h, self.conv_norm_out.weight, self.conv_norm_out.bias, self.cfg.norm_num_groups,
+                                  self.cfg.norm_eps, True)
+        out = K.conv2d(hn, self.conv_out.w_nhwc, bias=self.conv_out.bias)
+        if save:
+            rt.saved.append({"h": h, "st": st})
+        return out, rt
+
+    def backward_nhwc(self, dout, rt):
+        """Manual backward of forward_nhwc(save=True): accumulates LoRA grads into self.lora.grad.
+        Returns None (no gradient w.r.t. the latent input is needed on the hot path)."""
+        B = dout.shape[0]
+        sv = rt.saved.pop()
+        # conv_out input-gradient (C_out = 4): im2col of dout + GEMM with the rotated, transposed weights
+        _, H, W, _ = dout.shape
+        cols = K.im2col3(dout.contiguous(), self.conv_out.kp_dx)
+        dhn = K.gemm(cols, self.conv_out.w_dx_col).view(B, H, W, -1)
+        dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True)
+        skip_grads = []
+        for i in reversed(range(len(self.up_blocks))):
+            blk = self.up_blocks[i]
+            if hasattr(blk, "upsamplers"):
+                dh = blk.upsamplers[0].bwd(dh, rt)
+            for j in reversed(range(len(blk.resnets))):
+                if hasattr(blk, "attentions"):
+                    dh = blk.attentions[j].bwd(dh, rt, f"up_blocks.{i}.attentions.{j}")
+                dhc = blk.resnets[j].bwd(dh, rt)
+                c1 = rt.saved.pop()["c1"]
+                dh, ds = K.split_channels(dhc, c1)
+                skip_grads.append(ds)
+        m = self.mid_block
+        dh = m.resnets[1].bwd(dh, rt)
+        dh = m.attentions[0].bwd(dh, rt, "mid_block.attentions.0")
+        dh = m.resnets[0].bwd(dh, rt)
+        # the up-block backward visits skips in forward-push order, so the down-block backward takes them from the end
+        for i in reversed(range(len(self.down_blocks))):
+            blk = self.down_blocks[i]
+            if hasattr(blk, "downsamplers"):
+                dh = K.add(dh, skip_grads.pop())
+                dh = blk.downsamplers[0].bwd(dh, rt)
+            for j in reversed(range(len(blk.resnets))):
+                dh = K.add(dh, skip_grads.pop())
+                if hasattr(blk, "attentions"):
+                    dh = blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}")
+                dh = blk.resnets[j].bwd(dh, rt)
+        # remaining skip (conv_in output) -- conv_in has no trainable params and x needs no grad
+        assert len(skip_grads) == 1 and not rt.saved, (len(skip_grads), len(rt.saved))
+        return None
+
+    # ---------------- diffusers call surface ----------------
+    def forward(self, sample, timestep, encoder_hidden_states, added_cond_kwargs=None, return_dict=True, **kw):
+        added = added_cond_kwargs or {}
+        x = K.nchw_to_nhwc(sample)
+        need_grad = (torch.is_grad_enabled() and self.lora is not None and self._adapters_enabled)
+        if need_grad:
+            out = _UNetFn.apply(x, self.lora.param, self, timestep, encoder_hidden_states, added["text_embeds"],
+                                added["time_ids"])
+        else:
+            with torch.no_grad():
+                out, _ = self.forward_nhwc(x, timestep, encoder_hidden_states, added["text_embeds"],
+                                           added["time_ids"], save=False)
+        eps = _NHWC2NCHW.apply(out)
+        return _Output(sample=eps) if return_dict else (eps,)
+
+    __call__ = nn.Module.__call__
+
+
+class _UNetFn(torch.autograd.Function):
+    """The whole UNet as one autograd node; LoRA grads go straight into the flat grad buffer."""
+
+    @staticmethod
+    def forward(ctx, x, lora_param, unet, timestep, enc, text_embeds, time_ids):
+        out, rt = unet.forward_nhwc(x, timestep, enc, text_embeds, time_ids, save=True)
+        ctx.unet, ctx.rt = unet, rt
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ctx.unet.backward_nhwc(dout.contiguous(), ctx.rt)
+        ctx.rt = None
+        return None, None, None, None, None, None, None
+
+
+class _NHWC2NCHW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return K.nhwc_to_nchw(x, torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        return K.nchw_to_nhwc(g.contiguous())
