@@ -1,0 +1,185 @@
+"""PSO train-step throughput on MI355X (BASELINE.json metric: "PSO train-step imgs/sec (paired 1024^2 SDXL)").
+
+Workload (BASELINE.json configs[1]): SDXL-Turbo PSO, bf16, 1024x1024 (128x128 latents), 2-step
+sampler (T = 1 trained transition; a literal 1-step sampler trains nothing), LoRA r=32 grads only,
+2 pairs per micro-step per GPU, gradient_accumulation_steps 2 (the turbo config default).  One bench "step" = one
+optimizer step = gas*T micro-steps (+ the per-inner-epoch buffer shuffle, RCCL all-reduce, clip, AdamW); each
+micro-step trains 2P images (2P policy UNet fwd+bwd + 2P reference fwd + fused loss).  Synthetic data: random-init
+SDXL weights (seeded), N(0,1) text embeddings, trajectories from this build's own sampler (untimed), U(0,1)
+rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling), RCCL all-reduce of the flat LoRA grads.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (torchrun sets RANK/WORLD_SIZE/LOCAL_RANK)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+SURVEY_TFLOP_PER_PAIR_MICRO = {32: 42.54, 16: 42.29}  # LoRA @1024^2, excludes checkpoint recompute
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=2)
+    ap.add_argument("--gas", type=int, default=2)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--rank", type=int, default=32)
+    ap.add_argument("--num-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build(args, dev):
+    from types import SimpleNamespace
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    h = args.res // 8
+    with torch.device(dev):
+        unet = UNet2DConditionModel(UNetConfig.sdxl(h))
+    unet.init_weights(0)  # same frozen weights on every rank
+    unet.add_adapter(SimpleNamespace(r=args.rank, lora_alpha=args.rank))
+    unet.lora.init_gaussian(seed=0, b_std=1e-3)  # non-zero B so policy != reference
+    unet.prepare()
+    tr = PSOTrainer(unet, mode="turbo", num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
+                    train_batch_size=args.pairs, num_reward=1)
+    g = torch.Generator(device=dev).manual_seed(1000 + int(os.environ.get("RANK", "0")))
+    Bp = args.pairs * args.gas  # pairs sampled per epoch per GPU
+    enc = torch.randn(Bp, 77, 2048, device=dev, generator=g).bfloat16()
+    pooled = torch.randn(Bp, 1280, device=dev, generator=g).bfloat16()
+    tid = compute_time_ids(args.res, 0, dev).repeat(Bp, 1)
+    reward = lambda img: torch.rand(img.shape[0], device=dev, generator=g)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g, reward_fn=reward)
+    return unet, tr, buf, g
+
+
+def one_step(tr, buf, g):
+    sb = tr.shuffle(buf, generator=g)
+    tr.train_epoch(sb)
+
+
+def roofline(tr, buf, g):
+    """One extra profiled step: HIP events around every MFMA GEMM/conv launch (torch's current stream = the launch
+    stream).  achieved = sum of algorithmic 2*M*N*K over those launches / sum of their durations."""
+    from pairwise_sample_optimization_amd import kernels as K
+    K.PROFILE = []
+    one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    rec, K.PROFILE = K.PROFILE, None
+    fl = sum(f for f, _, _ in rec)
+    ms = sum(a.elapsed_time(b) for _, a, b in rec)
+    n = len(rec)
+    achieved = fl / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "gemm_bf16_kernel (all GEMM + implicit-GEMM conv launches)",
+            "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "launches_per_step": n,
+            "flop_per_step": fl, "avg_launch_us": round(ms * 1e3 / max(n, 1), 2)}
+
+
+def cpu_baseline(args, unet):
+    """Oracle (plain torch fp32 CPU restatement, oracle/sdxl_ref.py) on a bounded sample of the same workload: the
+    per-image share of one micro-step at 1024^2 = 1 policy forward + LoRA backward + 1 reference forward."""
+    from oracle import sdxl_ref
+    torch.set_num_threads(args.cpu_threads)
+    sd = {k: v.float().cpu() for k, v in unet.state_dict().items()}
+    lora = {k: v.float().cpu().requires_grad_(True) for k, v in unet.lora.state_dict_peft().items()}
+    h = args.res // 8
+    x = torch.randn(1, 4, h, h)
+    t = torch.tensor([999.0])
+    enc = torch.randn(1, 77, 2048)
+    pooled = torch.randn(1, 1280)
+    tid = torch.tensor([[args.res, args.res, 0, 0, args.res, args.res]], dtype=torch.float32)
+    t0 = time.perf_counter()
+    out = sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=lora)
+    out.sum().backward()
+    with torch.no_grad():
+        sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=None)
+    dt = time.perf_counter() - t0
+    del sd, lora
+    return {"value": round(1.0 / dt, 5), "unit": "imgs/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"1 image at {args.res}^2: policy fwd + LoRA bwd + reference fwd, fp32 torch oracle, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    torch.manual_seed(rank)
+    t_build = time.time()
+    unet, tr, buf, g = build(args, dev)
+    log(f"[bench] built + sampled in {time.time() - t_build:.1f}s; warmup {args.warmup}")
+    for _ in range(args.warmup):
+        one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    imgs_per_step_gpu = 2 * args.pairs * args.gas * (args.num_steps - 1)
+    value = imgs_per_step_gpu * world * args.steps / dt
+    ms = dt / args.steps * 1e3
+    loss = torch.stack(tr.loss_hist[-4:]).mean().item()
+    res = {
+        "metric": "PSO train-step imgs/sec (paired 1024² SDXL) at 1/2/4/8 MI355X",
+        "value": round(value, 3), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16", "data": "synthetic (random-init SDXL weights, N(0,1) text embeds, own-sampler trajectories)",
+        "config": {"workload": "C2: SDXL-Turbo PSO train step, LoRA r=%d grads, %d pairs/GPU/micro-step, gas %d, "
+                               "%d-step sampler (T=%d)" % (args.rank, args.pairs, args.gas, args.num_steps,
+                                                           args.num_steps - 1),
+                   "global_batch": 2 * args.pairs * world, "seq_len": (args.res // 16) ** 2, "resolution": args.res,
+                   "parallelism": f"dp{world}"},
+        "loss": round(loss, 6),
+    }
+    tf = SURVEY_TFLOP_PER_PAIR_MICRO.get(args.rank) if args.res == 1024 else None
+    if tf:
+        step_tf = tf * args.pairs * args.gas * (args.num_steps - 1)
+        res["step_mfma_frac"] = round(step_tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)
+    if not args.no_roofline:
+        res["roofline"] = roofline(tr, buf, g)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[bench] cpu baseline ...")
+        res["cpu_baseline"] = cpu_baseline(args, unet)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -178,12 +178,36 @@ int pso_cast_bf16_f32(long n, const void* x, float* y, void* stream);
 int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt, void* stream);
 /* channel concat of NHWC rows (torch.cat([h, skip], dim=1) of the up blocks) and its inverse; the split can add a
  * second gradient into the skip part (the skip tensor also feeds the next down layer). */
+/* batched transpose: descs = device array of n {const bf16* src; bf16* dst; int R, C; long ldi, ldo;} (src [R][C]
+ * -> dst [C][R]); one launch for all LoRA working-copy transposes after an optimizer step. */
+int pso_transpose_batched(int n, const void* descs, int max_r, int max_c, void* stream);
+/* dst row i = src row idx[i] (row_bytes % 4 == 0): the pair/time shuffles of the trajectory buffer (T:733-745) */
+int pso_gather_rows(long n, long row_bytes, const void* src, const int64_t* idx, void* dst, void* stream);
 /* layout conversion of the (small) latent tensors at the diffusers NCHW API boundary */
 int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream);
 int pso_nhwc_to_nchw(int B, int C, long HW, const void* src, void* dst, int dst_dtype, void* stream);
 int pso_concat_channels(long npix, int C1, const void* x1, int C2, const void* x2, void* out, void* stream);
 int pso_split_channels(long npix, int C1, int C2, const void* in, void* y1, void* y2, const void* add2,
                        void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Optimizer / clipping / preference (fp32, on device, no host synchronisation).
+ * pso_grad_clip_coef: out[0] = ||grad||_2 * grad_scale, out[1] = min(1, max_norm / (norm + 1e-6))
+ *   Replaces: accelerator.clip_grad_norm_(params_to_optimize, max_grad_norm)   T:858-859
+ * pso_adamw_step: torch.optim.AdamW semantics on (param, grad * grad_scale * clip_coef[1]); step counts from 1.
+ *   Replaces: optimizer.step() T:860 (AdamW; bitsandbytes AdamW8bit has no ROCm build here)
+ * pso_preference: rewards [P][2][m] -> pref [P][2]; mode 0 = sample_compare (T:401-416, reward column reward_idx[p]
+ *   or 0, ties -> member 0 loses), mode 1 = compare (D:420-434, strict Pareto, ties -> (0,0)).
+ * ---------------------------------------------------------------------------------------------------------------- */
+size_t pso_grad_clip_ws_bytes(long n);
+int pso_grad_clip_coef(long n, const float* grad, float grad_scale, float max_norm, float* out_norm_coef, void* ws,
+                       size_t ws_bytes, void* stream);
+int pso_adamw_step(long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, int step, float grad_scale, const float* clip_coef,
+                   void* stream);
+int pso_zero_f32(long n, float* x, void* stream);
+int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
+                   void* stream);
 
 #ifdef __cplusplus
 }

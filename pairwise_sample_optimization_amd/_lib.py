@@ -62,6 +62,13 @@ SIGNATURES = {
     "pso_conv_weight_t": (ci, [ci, ci, ci, ci, vp, vp, vp]),
     "pso_concat_channels": (ci, [cl, ci, vp, ci, vp, vp, vp]),
     "pso_nchw_to_nhwc": (ci, [ci, ci, cl, vp, ci, vp, vp]),
+    "pso_grad_clip_ws_bytes": (csz, [cl]),
+    "pso_transpose_batched": (ci, [ci, vp, ci, ci, vp]),
+    "pso_gather_rows": (ci, [cl, cl, vp, vp, vp, vp]),
+    "pso_grad_clip_coef": (ci, [cl, vp, cf, cf, vp, vp, csz, vp]),
+    "pso_adamw_step": (ci, [cl, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
+    "pso_zero_f32": (ci, [cl, vp, vp]),
+    "pso_preference": (ci, [ci, ci, vp, vp, ci, vp, vp]),
     "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),
     "pso_split_channels": (ci, [cl, ci, ci, vp, vp, vp, vp, vp]),
 }

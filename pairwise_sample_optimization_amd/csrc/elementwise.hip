@@ -263,7 +263,59 @@ __global__ void nhwc_to_nchw_kernel(int B, int C, long HW, const bf16_t* __restr
   }
 }
 
+// many small transposes in one launch: grid (64x64 tiles of the largest matrix, n matrices)
+struct TransposeDesc {
+  const bf16_t* src;
+  bf16_t* dst;
+  int R, C;
+  long ldi, ldo;
+};
+__global__ void transpose_batched_kernel(const TransposeDesc* __restrict__ d) {
+  __shared__ bf16_t tile[64][66];
+  const TransposeDesc t = d[blockIdx.z];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  if (r0 >= t.R || c0 >= t.C) return;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < t.R && c < t.C) ? t.src[(long)r * t.ldi + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < t.C && r < t.R) t.dst[(long)c * t.ldo + r] = tile[tx][i];
+  }
+}
+
+// dst[i] = src[idx[i]] for rows of `units` elements of type U (16-B units when the row size allows, else 4-B)
+template <typename U>
+__global__ void gather_rows_kernel(long n, long units, const U* __restrict__ src, const int64_t* __restrict__ idx,
+                                   U* __restrict__ dst) {
+  GRID_STRIDE(i, n * units) {
+    const long r = i / units, c = i - r * units;
+    dst[i] = src[idx[r] * units + c];
+  }
+}
+
 extern "C" {
+
+int pso_transpose_batched(int n, const void* descs, int max_r, int max_c, void* stream) {
+  PSO_ARG_CHECK(n > 0 && descs, "pso_transpose_batched: bad args");
+  dim3 grid(cdiv(max_c, 64), cdiv(max_r, 64), n);
+  transpose_batched_kernel<<<grid, 256, 0, (hipStream_t)stream>>>((const TransposeDesc*)descs);
+  return pso_check_launch("pso_transpose_batched");
+}
+
+int pso_gather_rows(long n, long row_bytes, const void* src, const int64_t* idx, void* dst, void* stream) {
+  PSO_ARG_CHECK(row_bytes % 4 == 0 && src && idx && dst, "pso_gather_rows: row_bytes %% 4");
+  if (row_bytes % 16 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0)
+    gather_rows_kernel<uint4><<<grid_for(n * (row_bytes / 16)), 256, 0, (hipStream_t)stream>>>(
+        n, row_bytes / 16, (const uint4*)src, idx, (uint4*)dst);
+  else
+    gather_rows_kernel<uint32_t><<<grid_for(n * (row_bytes / 4)), 256, 0, (hipStream_t)stream>>>(
+        n, row_bytes / 4, (const uint32_t*)src, idx, (uint32_t*)dst);
+  return pso_check_launch("pso_gather_rows");
+}
 
 int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream) {
   PSO_ARG_CHECK(src && dst && (src_dtype == PSO_F32 || src_dtype == PSO_BF16), "pso_nchw_to_nhwc: bad args");

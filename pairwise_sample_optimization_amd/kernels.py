@@ -12,6 +12,24 @@ from ._lib import check, lib, ptr, require_cuda, stream_ptr, dtype_code, PSO_BF1
 CONV_NORMAL, CONV_UP2, CONV_T2 = 1, 2, 3
 BF16 = torch.bfloat16
 
+# Optional per-launch accounting of the MFMA GEMM/conv kernel (bench.py roofline): list of (flops, ev0, ev1)
+PROFILE = None
+
+
+def _prof_begin():
+    if PROFILE is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return e0
+
+
+def _prof_end(e0, flops):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        PROFILE.append((flops, e0, e1))
+
 
 def _row_stride(t):
     assert t.dim() == 2 and t.stride(1) == 1, "operand must be a 2-D view with contiguous rows"
@@ -33,6 +51,7 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
         assert a2.shape[1] == (K2 * (N // tail_group_n) if tail_group_n else K2)
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=out_dtype)
+    e0 = _prof_begin()
     check(lib().pso_gemm(M, N, ptr(a), _row_stride(a), K1, ptr(w), _row_stride(w),
                          ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
                          ptr(w2), _row_stride(w2) if w2 is not None else 0,
@@ -40,6 +59,7 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
                          int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
                          ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
                          stream_ptr()), "pso_gemm")
+    _prof_end(e0, 2.0 * M * N * (K1 + K2))
     return out
 
 
@@ -67,12 +87,14 @@ def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=N
     K2 = a2.shape[1] if a2 is not None else 0
     o2 = out.view(B * Ho * Wo, -1) if out.is_contiguous() else None
     ldo = Cout if o2 is None else o2.stride(0)
+    e0 = _prof_begin()
     check(lib().pso_conv2d(mode, B, ptr(x), C1, ptr(x2), C2, H, W, Ho, Wo, ks, stride, pad, ptr(weight), Cout,
                            ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
                            ptr(w2), _row_stride(w2) if w2 is not None else 0, float(alpha), ptr(bias),
                            ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
                            ptr(resid), Cout if resid is not None else 0, ptr(out), ldo, dtype_code(out),
                            int(accumulate), stream_ptr()), "pso_conv2d")
+    _prof_end(e0, 2.0 * B * Ho * Wo * Cout * (ks * ks * (C1 + C2) + K2))
     return out
 
 
@@ -347,4 +369,72 @@ def nhwc_to_nchw(x, dtype=torch.float32):
     out = torch.empty((B, C, H, W), device=x.device, dtype=dtype)
     check(lib().pso_nhwc_to_nchw(B, C, H * W, ptr(x.contiguous()), ptr(out), dtype_code(out), stream_ptr()),
           "pso_nhwc_to_nchw")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# optimizer / clipping / preference
+# ------------------------------------------------------------------------------------------------------------------
+def grad_clip_coef(grad, max_norm, grad_scale=1.0, out=None):
+    """-> float32[2] device tensor (norm, clip coefficient)."""
+    n = grad.numel()
+    out = torch.empty(2, device=grad.device, dtype=torch.float32) if out is None else out
+    wsb = lib().pso_grad_clip_ws_bytes(n)
+    ws = torch.empty(wsb, device=grad.device, dtype=torch.uint8)
+    check(lib().pso_grad_clip_coef(n, ptr(grad), float(grad_scale), float(max_norm), ptr(out), ptr(ws), wsb,
+                                   stream_ptr()), "pso_grad_clip_coef")
+    return out
+
+
+def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None):
+    check(lib().pso_adamw_step(param.numel(), ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), float(lr),
+                               float(betas[0]), float(betas[1]), float(eps), float(weight_decay), int(step),
+                               float(grad_scale), ptr(clip), stream_ptr()), "pso_adamw_step")
+
+
+def zero_(x):
+    check(lib().pso_zero_f32(x.numel(), ptr(x), stream_ptr()), "pso_zero_f32")
+    return x
+
+
+def preference(rewards, mode, reward_idx=None, out=None):
+    """rewards [P, 2, m] fp32 -> pref [P, 2]."""
+    P, _, m = rewards.shape
+    out = torch.empty((P, 2), device=rewards.device, dtype=torch.float32) if out is None else out
+    check(lib().pso_preference(P, m, ptr(rewards.float().contiguous()), ptr(reward_idx), int(mode), ptr(out),
+                               stream_ptr()), "pso_preference")
+    return out
+
+
+class BatchedTranspose:
+    """A fixed list of (src [R,C], dst [C,R]) bf16 pairs transposed by ONE kernel launch (descriptor table on
+    device, built once: the buffers are persistent)."""
+
+    def __init__(self, pairs, device):
+        import numpy as np
+        dt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("R", "<i4"), ("C", "<i4"), ("ldi", "<i8"), ("ldo", "<i8")])
+        arr = np.zeros(len(pairs), dtype=dt)
+        self.max_r = self.max_c = 1
+        for i, (s, d) in enumerate(pairs):
+            R, C = s.shape
+            assert d.shape[0] == C and d.shape[1] >= R and s.stride(1) == 1 and d.stride(1) == 1
+            arr[i] = (s.data_ptr(), d.data_ptr(), R, C, s.stride(0), d.stride(0))
+            self.max_r, self.max_c = max(self.max_r, R), max(self.max_c, C)
+        self.n = len(pairs)
+        self.keep = pairs
+        self.desc = torch.from_numpy(arr.view(np.uint8)).to(device)
+
+    def __call__(self):
+        if self.n:
+            check(lib().pso_transpose_batched(self.n, ptr(self.desc), self.max_r, self.max_c, stream_ptr()),
+                  "pso_transpose_batched")
+
+
+def gather_rows(src, idx, out=None):
+    """out[i] = src[idx[i]] along dim 0 (rows of src[0].nbytes bytes)."""
+    n = idx.numel()
+    row_bytes = src[0].numel() * src.element_size()
+    out = torch.empty((n,) + tuple(src.shape[1:]), device=src.device, dtype=src.dtype) if out is None else out
+    check(lib().pso_gather_rows(n, row_bytes, ptr(src.contiguous()), ptr(idx.to(torch.int64).contiguous()),
+                                ptr(out), stream_ptr()), "pso_gather_rows")
     return out

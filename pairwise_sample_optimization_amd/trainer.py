@@ -1,0 +1,245 @@
+"""The online PSO epoch for timestep-distilled SDXL, MI355X-native: paired on-policy sampling, trajectory buffer +
+shuffles, the (pair-batch, transition) micro-step and the optimizer step.
+
+Reference loop (`T` = human_preference_tuning/train_online_pso_sdxl_turbo.py, `D` = ..._dmd2.py):
+  SAMPLING  T:554-673 / D:557-679  two independent trajectories per prompt through the distilled UNet, rewards
+  BUFFER    T:610-666,714-749       stack (B, 2, T, ...); per inner epoch permute pairs and, independently per pair,
+                                    the transition order (same for both members)
+  MICRO     T:771-861 / D:773-864   2 policy UNet fwd (LoRA on) + 2 reference fwd (adapters off) + 4 step log-probs
+                                    + clipped pairwise loss + backward; grads accumulate over gas*T micro-steps
+  SYNC      T:857-861               DDP all-reduce, clip_grad_norm_(1.0), optimizer.step, zero_grad
+
+Here every per-element operation runs in libpso_amd; the micro-step issues no host synchronisation (the reference
+syncs 4x in turbo_step_with_logprob's `.item()` lookups and once in `accelerator.gather(loss).item()`).  The two
+members of every pair ride in ONE UNet batch (image order 2p + k), policy and reference forwards share the frozen
+weights, the loss kernel consumes the bf16 NHWC eps directly and emits d loss / d eps for the hand-written UNet
+backward, which accumulates LoRA grads into the flat all-reduce bucket.
+"""
+import math
+from types import SimpleNamespace
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+from . import pso_core
+from ._lib import MODE_TURBO, MODE_DMD
+from .schedulers import EulerAncestralDiscreteScheduler, LCMScheduler, dmd_distill_timesteps
+
+BF16 = torch.bfloat16
+
+
+def compute_time_ids(size, crop=0, device=None):
+    """T:324-332 (512) / D:347-355 (1024): [orig_h, orig_w, crop_top, crop_left, target_h, target_w]."""
+    return torch.tensor([[size, size, crop, crop, size, size]], dtype=torch.float32, device=device)
+
+
+class PSOTrainer:
+    def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
+                 weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
+                 train_batch_size=1, num_reward=1, process_group=None):
+        self.unet = unet
+        self.mode = MODE_TURBO if mode == "turbo" else MODE_DMD
+        self.num_steps = num_steps
+        self.T = num_steps - 1                       # the last (deterministic) step is never trained (T:218-221)
+        self.beta, self.clip_eps = beta, clip_eps
+        self.lr, self.betas, self.wd, self.adam_eps = lr, betas, weight_decay, adam_eps
+        self.max_grad_norm = max_grad_norm
+        self.gas = gradient_accumulation_steps
+        self.gas_total = gradient_accumulation_steps * self.T  # Accelerator(gradient_accumulation_steps=gas*T) T:232
+        self.P = train_batch_size
+        self.m = num_reward
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        st = unet.lora
+        self.exp_avg = torch.zeros_like(st.master)
+        self.exp_avg_sq = torch.zeros_like(st.master)
+        self.opt_step = 0
+        self.n_micro = 0
+        self.clip_buf = torch.zeros(2, device=st.master.device, dtype=torch.float32)
+        self.loss_hist = []
+        self.auto_step = True  # run the optimizer every gas*T micro-steps (tests may inspect raw grads)
+        if self.mode == MODE_TURBO:
+            self.sched = EulerAncestralDiscreteScheduler()
+            self.sched.set_timesteps(num_steps)
+            self.timesteps = self.sched.timesteps.clone()  # float32 [N]
+        else:
+            self.sched = LCMScheduler()
+            ts, self.step_ratio = dmd_distill_timesteps(num_steps)
+            self.timesteps = ts.float()
+        dev = st.master.device
+        self.timesteps_dev = self.timesteps.to(dev)
+        # per-transition step coefficients [T, 8], host-computed once, device resident
+        self.coef_dev = torch.stack([self.coef_for_step(j, 1)[0] for j in range(self.T)], 0).to(dev) \
+            if self.T > 0 else torch.zeros(0, 8, device=dev)
+
+    # ------------------------------------------------------------------------------------------------------------
+    # coefficients of transition j (host float32 scalars, the reference's operation order)
+    # ------------------------------------------------------------------------------------------------------------
+    def coef_for_step(self, j, n):
+        if self.mode == MODE_TURBO:
+            t = self.timesteps[j].repeat(n)
+            return pso_core.turbo_coef(self.sched.sigmas, self.sched.timesteps, t)
+        t = self.timesteps[j].long().repeat(n)
+        return pso_core.dmd_coef(self.sched.alphas_cumprod, t, t - self.step_ratio)
+
+    # ------------------------------------------------------------------------------------------------------------
+    # SAMPLING: B prompts -> 2 trajectories each (independent x_T, T:572-608) -> buffer rows
+    # ------------------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def sample_pairs(self, enc, pooled, time_ids, h, generator=None, reward_fn=None, decode_fn=None):
+        """enc [B,77,Dc] bf16, pooled [B,Dp], time_ids [B,6].  Returns a dict of NHWC buffer tensors.
+        Both trajectories of a prompt are sampled in ONE UNet batch (image order 2b + k)."""
+        dev = enc.device
+        B = enc.shape[0]
+        n_img = 2 * B
+        N, T = self.num_steps, self.T
+        enc2 = enc.repeat_interleave(2, 0).contiguous()
+        pooled2 = pooled.repeat_interleave(2, 0).contiguous()
+        tid2 = time_ids.repeat_interleave(2, 0).contiguous()
+        shape = (n_img, h, h, 4)
+        x = torch.randn(shape, device=dev, generator=generator, dtype=torch.float32)
+        if self.mode == MODE_TURBO:
+            x = x * float(self.sched.init_noise_sigma)
+        xs, ins, lps = [x], [], []
+        for i in range(N):
+            t = self.timesteps_dev[i].repeat(n_img)
+            if self.mode == MODE_TURBO:
+                sig = float(self.sched.sigmas[i])
+                model_in = K.cast_f32_bf16(x, scale=1.0 / math.sqrt(sig * sig + 1.0))  # DP/sdxl_turbo...:120-122
+            else:
+                model_in = K.cast_f32_bf16(x)
+            eps, _ = self.unet.forward_nhwc(model_in, t, enc2, pooled2, tid2, save=False)
+            if i < N - 1:
+                coef = self.coef_for_step(i, n_img).to(dev)
+                if self.mode == MODE_TURBO:
+                    noise = torch.randn(shape, device=dev, generator=generator)
+                    x, lp = K.step_logprob(self.mode, x, eps, coef, noise=noise)
+                else:  # DMD2: one (1,C,H,W) draw shared across the batch (DP/distilled_...:123-126)
+                    noise = torch.randn((1,) + shape[1:], device=dev, generator=generator)
+                    x, lp = K.step_logprob(self.mode, x, eps, coef, noise=noise, noise_shared=True)
+                xs.append(x)
+                ins.append(model_in)
+                lps.append(lp)
+            else:
+                x_final = self._final_step(x, eps, n_img)
+        x_stack = torch.stack(xs[:T + 1], 1)                    # [2B, T+1, h, h, 4]
+        buf = dict(x=x_stack[:, :T].contiguous(), x_next=x_stack[:, 1:T + 1].contiguous(),
+                   unet_in=torch.stack(ins, 1).contiguous(), lp=torch.stack(lps, 1), enc=enc2, pooled=pooled2,
+                   tid=tid2)
+        buf["x_final"] = x_final
+        if reward_fn is not None:
+            img = decode_fn(x_final) if decode_fn is not None else x_final
+            buf["rewards"] = reward_fn(img).reshape(B, 2, -1).float()
+        return buf
+
+    def _final_step(self, x, eps, n):
+        """Last sampler step (never trained): turbo sigma_to = 0 -> x + eps*(0 - sigma) (T:218-221); DMD2 returns
+        x0 = (x - sqrt(1-a_t) eps) / sqrt(a_t) (DP/sdxl_dmd_with_logprob.py:154-162)."""
+        dev = x.device
+        zero = torch.zeros((1,) + tuple(x.shape[1:]), device=dev)
+        if self.mode == MODE_TURBO:
+            c = self.coef_for_step(self.num_steps - 1, n)
+        else:
+            t = self.timesteps[-1].long().repeat(n)
+            c = pso_core.dmd_coef(self.sched.alphas_cumprod, t, t)
+            c[:, 2] = 1.0  # sqrt(abar_prev) -> 1: mean = x0
+            c[:, 3] = 1.0
+        xf, _ = K.step_logprob(self.mode, x, eps, c.to(dev), noise=zero, noise_shared=True)
+        return xf
+
+    # ------------------------------------------------------------------------------------------------------------
+    # BUFFER shuffle (T:733-749): pair permutation + independent per-pair transition permutation, written out in
+    # micro-step order so every micro-step reads contiguous [2P] slices.
+    # ------------------------------------------------------------------------------------------------------------
+    def shuffle(self, buf, generator=None):
+        dev = buf["x"].device
+        n_img = buf["x"].shape[0]
+        Bp = n_img // 2
+        T, P = self.T, self.P
+        assert Bp % P == 0, "samples per epoch must be a multiple of train.batch_size (T:521-523)"
+        perm = torch.randperm(Bp, device=dev, generator=generator)
+        perms = torch.argsort(torch.rand((Bp, T), device=dev, generator=generator), dim=1)  # per-pair time perm
+        nb = Bp // P
+        pb = torch.arange(nb, device=dev).view(nb, 1, 1, 1)
+        jj = torch.arange(T, device=dev).view(1, T, 1, 1)
+        pp = torch.arange(P, device=dev).view(1, 1, P, 1)
+        kk = torch.arange(2, device=dev).view(1, 1, 1, 2)
+        pair = perm[pb * P + pp]                                  # [nb,1,P,1]
+        tsel = perms[pair, jj]                                    # [nb,T,P,1]
+        img_idx = ((pair * 2 + kk) * T + tsel).reshape(-1)        # rows of [2Bp*T]
+        pair_img = (pair * 2 + kk).expand(nb, T, P, 2).reshape(-1)  # rows of [2Bp]
+        tsel_i = tsel.expand(nb, T, P, 2).reshape(-1)
+        tt = self.timesteps_dev[tsel_i]
+        out = SimpleNamespace(n_micro=nb * T, P=P)
+        flat = lambda t: t.reshape((n_img * T,) + tuple(t.shape[2:]))
+        out.x = K.gather_rows(flat(buf["x"]), img_idx)
+        out.x_next = K.gather_rows(flat(buf["x_next"]), img_idx)
+        out.unet_in = K.gather_rows(flat(buf["unet_in"]), img_idx)
+        out.enc = K.gather_rows(buf["enc"], pair_img)
+        out.pooled = K.gather_rows(buf["pooled"], pair_img)
+        out.tid = K.gather_rows(buf["tid"], pair_img)
+        out.t = tt.float().contiguous()
+        out.coef = K.gather_rows(self.coef_dev, tsel_i)               # per-image step coefficients
+        rw = buf["rewards"]                                       # [Bp, 2, m]
+        out.rewards = rw[perm[(torch.arange(nb, device=dev)[:, None] * P + torch.arange(P, device=dev)[None])]]
+        out.rewards = out.rewards.reshape(nb, 1, P, 2, -1).expand(nb, T, P, 2, rw.shape[-1]).reshape(-1, 2,
+                                                                                                   rw.shape[-1])
+        out.rewards = out.rewards.contiguous()
+        return out
+
+    def micro_batch(self, sb, s):
+        n = 2 * self.P
+        sl = slice(s * n, (s + 1) * n)
+        return SimpleNamespace(x=sb.x[sl], x_next=sb.x_next[sl], unet_in=sb.unet_in[sl], enc=sb.enc[sl],
+                               pooled=sb.pooled[sl], tid=sb.tid[sl], t=sb.t[sl], coef=sb.coef[sl],
+                               rewards=sb.rewards[s * self.P:(s + 1) * self.P])
+
+    # ------------------------------------------------------------------------------------------------------------
+    # MICRO-STEP (T:773-861) -- no host synchronisation
+    # ------------------------------------------------------------------------------------------------------------
+    def micro_step(self, mb, generator=None):
+        u = self.unet
+        u.enable_adapters()
+        eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
+        u.disable_adapters()
+        with torch.no_grad():
+            eps_ref, _ = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
+        u.enable_adapters()
+        idx = None
+        if self.mode == MODE_TURBO and self.m > 1:  # sample_compare draws a reward column per pair (T:405)
+            idx = torch.randint(0, self.m, (self.P,), device=mb.x.device, generator=generator)
+        pref = K.preference(mb.rewards, 0 if self.mode == MODE_TURBO else 1, reward_idx=idx)
+        ws = K.pair_loss_ws(self.P, mb.x[0].numel(), mb.x.device)
+        loss, lp = K.pair_loss_fwd(self.mode, mb.x, mb.x_next, eps_pol, eps_ref, mb.coef, pref, self.beta,
+                                   self.clip_eps, ws)
+        # accelerator.backward divides by gradient_accumulation_steps (accelerate accelerator.py:2840)
+        deps = K.pair_loss_bwd(self.mode, mb.x, mb.x_next, eps_pol, mb.coef, pref, self.beta, self.clip_eps, ws,
+                               grad_scale=1.0 / self.gas_total)
+        u.backward_nhwc(deps, rt)
+        self.loss_hist.append(loss)
+        self.n_micro += 1
+        if self.auto_step and self.n_micro % self.gas_total == 0:
+            self.optimizer_step()
+        return loss
+
+    # ------------------------------------------------------------------------------------------------------------
+    # SYNC (T:857-861): all-reduce (RCCL) -> clip -> AdamW -> zero -> refresh bf16 working copies
+    # ------------------------------------------------------------------------------------------------------------
+    def optimizer_step(self):
+        st = self.unet.lora
+        scale = 1.0
+        if self.world > 1:
+            dist.all_reduce(st.grad, group=self.pg)  # one flat bucket over xGMI; mean folded into grad_scale
+            scale = 1.0 / self.world
+        K.grad_clip_coef(st.grad, self.max_grad_norm, grad_scale=scale, out=self.clip_buf)
+        self.opt_step += 1
+        K.adamw_step(st.master, st.grad, self.exp_avg, self.exp_avg_sq, self.lr, self.betas, self.adam_eps, self.wd,
+                     self.opt_step, grad_scale=scale, clip=self.clip_buf)
+        K.zero_(st.grad)
+        st.refresh()
+
+    def train_epoch(self, sb):
+        """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861)."""
+        for s in range(sb.n_micro):
+            self.micro_step(self.micro_batch(sb, s))

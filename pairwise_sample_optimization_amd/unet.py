@@ -78,6 +78,12 @@ def _param(*shape):
     return nn.Parameter(torch.empty(*shape, dtype=BF16), requires_grad=False)
 
 
+def _uniform_(p, bound, g):
+    """U(-bound, bound) on the parameter's own device (PyTorch-default-style fan-in init, synthetic weights)."""
+    with torch.no_grad():
+        p.copy_((torch.rand(p.shape, generator=g, device=p.device, dtype=torch.float32) * 2 - 1) * bound)
+
+
 class Linear(nn.Module):
     def __init__(self, fin, fout, bias=True):
         super().__init__()
@@ -87,10 +93,9 @@ class Linear(nn.Module):
 
     def reset(self, g):
         bound = 1.0 / math.sqrt(self.in_features)
-        with torch.no_grad():
-            self.weight.copy_((torch.rand(self.weight.shape, generator=g) * 2 - 1) * bound)
-            if self.bias is not None:
-                self.bias.copy_((torch.rand(self.bias.shape, generator=g) * 2 - 1) * bound)
+        _uniform_(self.weight, bound, g)
+        if self.bias is not None:
+            _uniform_(self.bias, bound, g)
 
     def prepare(self):
         self.wt = K.transpose(self.weight.data)  # [in][out] for the input gradient
@@ -105,10 +110,9 @@ class Conv2d(nn.Module):
 
     def reset(self, g):
         bound = 1.0 / math.sqrt(self.cin * self.k * self.k)
-        with torch.no_grad():
-            self.weight.copy_((torch.rand(self.weight.shape, generator=g) * 2 - 1) * bound)
-            if self.bias is not None:
-                self.bias.copy_((torch.rand(self.bias.shape, generator=g) * 2 - 1) * bound)
+        _uniform_(self.weight, bound, g)
+        if self.bias is not None:
+            _uniform_(self.bias, bound, g)
 
     def prepare(self):
         w = self.weight.data
@@ -148,33 +152,96 @@ class Norm(nn.Module):
 # ======================================================================================================================
 class LoraState:
     """peft LoraConfig(r, lora_alpha=r, init_lora_weights="gaussian", target_modules=[to_k,to_q,to_v,to_out.0])
-    (T:338-345): A ~ N(0, 1/r) [r, in], B = 0 [out, r], scaling alpha/r.  Entries are laid out in reverse forward
-    order, i.e. the order the backward produces their gradients (for bucketed all-reduce)."""
+    (T:338-345): A ~ N(0, 1/r) [r, in], B = 0 [out, r], scaling alpha/r.
 
-    def __init__(self, entries, r, alpha, device):
+    Storage: ONE flat fp32 master, ONE flat fp32 grad (the all-reduce bucket / optimizer operand), ONE flat bf16
+    working copy.  Transformer blocks are laid out in reverse forward order (the order the backward finishes their
+    gradients); inside a block the adapters that are used together are adjacent so their stacks are plain views:
+      attn1: [A_q A_k A_v] (3r x C) [B_q B_k B_v] (3C x r) A_o B_o | attn2: A_q B_q [A_k A_v] [B_k B_v] A_o B_o
+    After each optimizer step `refresh()` = one cast kernel + one batched-transpose kernel for the transposed forms the
+    backward GEMMs need (A^T, (sB)^T)."""
+
+    def __init__(self, blocks, r, alpha, device):
         self.r, self.alpha, self.scale = r, alpha, alpha / r
-        self.entries = entries  # list of (name, fin, fout) in forward order
-        self.index = {}
+        self.blocks = blocks  # [(path, C, Dc)] forward order
+        self.layout = {}
         off = 0
-        for name, fin, fout in reversed(entries):
-            self.index[name] = (off, fin, fout)
-            off += r * fin + fout * r
+        for path, C, Dc in reversed(blocks):
+            segs = {}
+            for key, rows, cols in (("attn1.A_qkv", 3 * r, C), ("attn1.B_qkv", 3 * C, r), ("attn1.A_o", r, C),
+                                    ("attn1.B_o", C, r), ("attn2.A_q", r, C), ("attn2.B_q", C, r),
+                                    ("attn2.A_kv", 2 * r, Dc), ("attn2.B_kv", 2 * C, r), ("attn2.A_o", r, C),
+                                    ("attn2.B_o", C, r)):
+                segs[key] = (off, rows, cols)
+                off += rows * cols
+            self.layout[path] = segs
         self.numel = off
         self.master = torch.zeros(off, device=device, dtype=torch.float32)
         self.grad = torch.zeros(off, device=device, dtype=torch.float32)
-        self.work = torch.zeros(off, device=device, dtype=BF16)  # bf16 copy (B pre-scaled)
+        self.work = torch.zeros(off, device=device, dtype=BF16)
         self.param = nn.Parameter(self.master, requires_grad=True)  # autograd trigger for the UNet node
-        self.cache = {}
+        self.blk = {}
+        pairs = []
+        for path, C, Dc in blocks:
+            w = lambda k: self.seg(self.work, path, k)
+            ns = SimpleNamespace()
+            ns.A_qkv, ns.sB_qkv, ns.A_o1, ns.sB_o1 = w("attn1.A_qkv"), w("attn1.B_qkv"), w("attn1.A_o"), w("attn1.B_o")
+            ns.A_q2, ns.sB_q2, ns.A_kv2, ns.sB_kv2 = w("attn2.A_q"), w("attn2.B_q"), w("attn2.A_kv"), w("attn2.B_kv")
+            ns.A_o2, ns.sB_o2 = w("attn2.A_o"), w("attn2.B_o")
+            ns.At_qkv = torch.empty(C, 3 * r, device=device, dtype=BF16)
+            ns.sBt_qkv = torch.empty(r, 3 * C, device=device, dtype=BF16)
+            ns.At_o1 = torch.empty(C, r, device=device, dtype=BF16)
+            ns.sBt_o1 = torch.empty(r, C, device=device, dtype=BF16)
+            ns.At_q2 = torch.empty(C, r, device=device, dtype=BF16)
+            ns.sBt_q2 = torch.empty(r, C, device=device, dtype=BF16)
+            ns.sBt_kv2 = torch.empty(r, 2 * C, device=device, dtype=BF16)
+            ns.At_o2 = torch.empty(C, r, device=device, dtype=BF16)
+            ns.sBt_o2 = torch.empty(r, C, device=device, dtype=BF16)
+            pairs += [(ns.A_qkv, ns.At_qkv), (ns.sB_qkv, ns.sBt_qkv), (ns.A_o1, ns.At_o1), (ns.sB_o1, ns.sBt_o1),
+                      (ns.A_q2, ns.At_q2), (ns.sB_q2, ns.sBt_q2), (ns.sB_kv2, ns.sBt_kv2), (ns.A_o2, ns.At_o2),
+                      (ns.sB_o2, ns.sBt_o2)]
+            self.blk[path] = ns
+        self._transposes = K.BatchedTranspose(pairs, device) if device.type == "cuda" else None
+        self._b_views = [self.seg(self.work, p, k) for p, _, _ in blocks for k in self.layout[p] if ".B_" in k]
 
-    def views(self, t, name):
-        off, fin, fout = self.index[name]
+    def seg(self, t, path, key):
+        off, rows, cols = self.layout[path][key]
+        return t[off:off + rows * cols].view(rows, cols)
+
+    # peft per-adapter views (A [r][in], B [out][r]) of a flat tensor
+    def adapter_views(self, t, name):
+        path, attn, mod = name.rsplit(".", 2)[0], name.rsplit(".", 2)[1], name.rsplit(".", 2)[2]
+        if mod == "0":  # to_out.0
+            path, attn = name.rsplit(".", 3)[0], name.rsplit(".", 3)[1]
+            mod = "to_out.0"
         r = self.r
-        return t[off:off + r * fin].view(r, fin), t[off + r * fin:off + r * fin + fout * r].view(fout, r)
+        if attn == "attn1":
+            if mod in ("to_q", "to_k", "to_v"):
+                j = ("to_q", "to_k", "to_v").index(mod)
+                A = self.seg(t, path, "attn1.A_qkv")[j * r:(j + 1) * r]
+                Bm = self.seg(t, path, "attn1.B_qkv")
+                C = Bm.shape[0] // 3
+                return A, Bm[j * C:(j + 1) * C]
+            return self.seg(t, path, "attn1.A_o"), self.seg(t, path, "attn1.B_o")
+        if mod == "to_q":
+            return self.seg(t, path, "attn2.A_q"), self.seg(t, path, "attn2.B_q")
+        if mod in ("to_k", "to_v"):
+            j = ("to_k", "to_v").index(mod)
+            Bm = self.seg(t, path, "attn2.B_kv")
+            C = Bm.shape[0] // 2
+            return self.seg(t, path, "attn2.A_kv")[j * r:(j + 1) * r], Bm[j * C:(j + 1) * C]
+        return self.seg(t, path, "attn2.A_o"), self.seg(t, path, "attn2.B_o")
+
+    def adapter_names(self):
+        for path, _, _ in self.blocks:
+            for a in ("attn1", "attn2"):
+                for m in ("to_q", "to_k", "to_v", "to_out.0"):
+                    yield f"{path}.{a}.{m}"
 
     def init_gaussian(self, seed=0, b_std=0.0):
         g = torch.Generator(device="cpu").manual_seed(seed)
-        for name, fin, fout in self.entries:
-            A, B = self.views(self.master, name)
+        for name in self.adapter_names():
+            A, B = self.adapter_views(self.master, name)
             A.copy_(torch.randn(A.shape, generator=g) / self.r)  # peft gaussian: std 1/r
             if b_std:
                 B.copy_(torch.randn(B.shape, generator=g) * b_std)
@@ -183,32 +250,36 @@ class LoraState:
         self.refresh()
 
     def refresh(self):
-        """bf16 working copies and transposed forms after a master update (one cast + per-adapter transposes)."""
+        """bf16 working copies (B pre-scaled by alpha/r) and their transposed forms after a master update."""
         K.cast_f32_bf16(self.master, out=self.work)
         if self.scale != 1.0:
-            for name in self.index:
-                _, Bw = self.views(self.work, name)
-                K.axpby(self.scale, Bw.contiguous(), out=Bw)
-        self.cache = {}
-        for name in self.index:
-            A, B = self.views(self.work, name)
-            self.cache[name] = SimpleNamespace(A=A, sB=B, At=K.transpose(A), sBt=K.transpose(B))
+            for Bw in self._b_views:
+                K.axpby(self.scale, Bw, out=Bw)
+        self._transposes()
 
-    def grad_views(self, name):
-        return self.views(self.grad, name)
+    def grad_seg(self, path, key):
+        return self.seg(self.grad, path, key)
 
     def state_dict_peft(self):
         """{module_path.lora_A.weight, module_path.lora_B.weight} (get_peft_model_state_dict naming)."""
         out = {}
-        for name in self.index:
-            A, B = self.views(self.master, name)
+        for name in self.adapter_names():
+            A, B = self.adapter_views(self.master, name)
             out[f"{name}.lora_A.weight"] = A.detach().clone()
             out[f"{name}.lora_B.weight"] = B.detach().clone()
         return out
 
+    def grad_dict_peft(self):
+        out = {}
+        for name in self.adapter_names():
+            A, B = self.adapter_views(self.grad, name)
+            out[f"{name}.lora_A.weight"] = A
+            out[f"{name}.lora_B.weight"] = B
+        return out
+
     def load_peft(self, sd):
-        for name in self.index:
-            A, B = self.views(self.master, name)
+        for name in self.adapter_names():
+            A, B = self.adapter_views(self.master, name)
             A.copy_(sd[f"{name}.lora_A.weight"])
             B.copy_(sd[f"{name}.lora_B.weight"])
         self.refresh()
@@ -219,12 +290,9 @@ def _T(x, pad_to=8):
     return K.transpose(x, pad_rows_to=pad_to)
 
 
-def _lora_dw(st, name, v, x, dy, u):
-    """LoRA parameter gradients, accumulated into the flat fp32 grad buffer:
-    dA[r][in] += v^T x ,  dB[out][r] += s * dy^T u   (v = dy (sB), u = x A^T)."""
-    gA, gB = st.grad_views(name)
-    K.gemm(_T(v), _T(x), out=gA, out_dtype=torch.float32, accumulate=True)
-    K.gemm(_T(dy), _T(u), out=gB, out_dtype=torch.float32, accumulate=True, alpha=st.scale)
+def _dw(out, a_t, b_t, alpha=1.0):
+    """out[f32] += alpha * a_t . b_t^T  with both operands already transposed ([rows][Mp], [cols][Mp])."""
+    K.gemm(a_t, b_t, out=out, out_dtype=torch.float32, accumulate=True, alpha=alpha)
 
 
 # ======================================================================================================================
@@ -266,30 +334,19 @@ class BasicTransformerBlock(nn.Module):
         self.attn2.prepare(False)
         self.ff.prepare()
 
-    def lora_entries(self, path):
-        e = []
-        for an, a in (("attn1", self.attn1), ("attn2", self.attn2)):
-            for tn, fin in (("to_q", a.dim), ("to_k", a.kv_dim), ("to_v", a.kv_dim), ("to_out.0", a.dim)):
-                e.append((f"{path}.{an}.{tn}", fin, a.dim))
-        return e
-
     def fwd(self, x, rt, path):
         """x [M, C] (M = B*S).  Returns h3 [M, C]."""
         C, M, B = self.dim, x.shape[0], rt.B
         S = M // B
         a1m, a2m = self.attn1, self.attn2
         lo = rt.lora_on
-        L = (lambda n: rt.lora.cache[f"{path}.{n}"]) if lo else None
-        sv = {} if rt.save else None
-        # --- self attention ---
+        L = rt.lora.blk[path] if lo else None
+        r = rt.r
+        # --- self attention: fused q/k/v projection, the three LoRA up-projections as a grouped K-tail ---
         n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
         if lo:
-            lq, lk, lv = L("attn1.to_q"), L("attn1.to_k"), L("attn1.to_v")
-            u_qkv = torch.empty((M, 3 * rt.r), device=x.device, dtype=BF16)
-            for j, l in enumerate((lq, lk, lv)):
-                K.gemm(n1, l.A, out=u_qkv[:, j * rt.r:(j + 1) * rt.r])
-            sB = rt.lora_qkv_sB[path]
-            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=sB, tail_group_n=C)
+            u_qkv = K.gemm(n1, L.A_qkv)                                     # [M, 3r]
+            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C)
         else:
             qkv = K.gemm(n1, a1m.w_qkv)
         q3 = qkv.view(B, S, 3 * C)
@@ -297,23 +354,19 @@ class BasicTransformerBlock(nn.Module):
         a1 = a1.view(M, C)
         o1 = a1m.to_out[0]
         if lo:
-            lo1 = L("attn1.to_out.0")
-            u_o1 = K.gemm(a1, lo1.A)
-            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=lo1.sB)
+            u_o1 = K.gemm(a1, L.A_o1)
+            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1)
         else:
             h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x)
-        # --- cross attention ---
+        # --- cross attention over the 77 text tokens ---
         n2, st2 = K.layer_norm_fwd(h1, self.norm2.weight, self.norm2.bias, 1e-5)
         enc = rt.enc  # [B*77, Dc]
         Se = enc.shape[0] // B
         if lo:
-            lq2, lk2, lv2 = L("attn2.to_q"), L("attn2.to_k"), L("attn2.to_v")
-            u_q2 = K.gemm(n2, lq2.A)
-            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=lq2.sB)
-            u_kv2 = torch.empty((enc.shape[0], 2 * rt.r), device=x.device, dtype=BF16)
-            K.gemm(enc, lk2.A, out=u_kv2[:, :rt.r])
-            K.gemm(enc, lv2.A, out=u_kv2[:, rt.r:])
-            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=rt.lora_kv_sB[path], tail_group_n=C)
+            u_q2 = K.gemm(n2, L.A_q2)
+            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2)
+            u_kv2 = K.gemm(enc, L.A_kv2)                                    # [B*77, 2r]
+            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=L.sB_kv2, tail_group_n=C)
         else:
             q2 = K.gemm(n2, a2m.to_q.weight)
             kv2 = K.gemm(enc, a2m.w_kv)
@@ -322,9 +375,8 @@ class BasicTransformerBlock(nn.Module):
         a2 = a2.view(M, C)
         o2 = a2m.to_out[0]
         if lo:
-            lo2 = L("attn2.to_out.0")
-            u_o2 = K.gemm(a2, lo2.A)
-            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=lo2.sB)
+            u_o2 = K.gemm(a2, L.A_o2)
+            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2)
         else:
             h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
         # --- GEGLU feed-forward ---
@@ -332,8 +384,8 @@ class BasicTransformerBlock(nn.Module):
         f = K.gemm(n3, self.ff.proj.weight, bias=self.ff.proj.bias)
         gg = K.geglu_fwd(f)
         h3 = K.gemm(gg, self.ff.out.weight, bias=self.ff.out.bias, resid=h2)
-        if sv is not None:
-            sv.update(x=x, st1=st1, n1=n1, qkv=qkv, a1=a1, lse1=lse1, h1=h1, st2=st2, n2=n2, q2=q2, kv2=kv2, a2=a2,
+        if rt.save:
+            sv = dict(x=x, st1=st1, n1=n1, qkv=qkv, a1=a1, lse1=lse1, h1=h1, st2=st2, n2=n2, q2=q2, kv2=kv2, a2=a2,
                       lse2=lse2, h2=h2, st3=st3, f=f)
             if lo:
                 sv.update(u_qkv=u_qkv, u_o1=u_o1, u_q2=u_q2, u_kv2=u_kv2, u_o2=u_o2)
@@ -348,20 +400,22 @@ class BasicTransformerBlock(nn.Module):
         r = rt.r
         lo = rt.lora_on
         st = rt.lora
-        L = (lambda n: st.cache[f"{path}.{n}"]) if lo else None
+        L = st.blk[path] if lo else None
+        g = (lambda k: st.grad_seg(path, k)) if lo else None
         a1m, a2m = self.attn1, self.attn2
         # --- FF ---
         dg = K.gemm(dh3, self.ff.out.wt)
         df = K.geglu_bwd(sv["f"], dg)
         dn3 = K.gemm(df, self.ff.proj.wt)
         dh2 = K.layer_norm_bwd(sv["h2"], dn3, sv["st3"], self.norm3.weight, dadd=dh3)
-        # --- cross attention out-proj ---
+        # --- cross attention out-proj:  y = a W^T + (a A^T)(sB)^T ;  v = dy sB ; da = dy W + v A ---
         o2 = a2m.to_out[0]
         if lo:
-            lo2 = L("attn2.to_out.0")
-            v_o2 = K.gemm(dh2, lo2.sBt)
-            da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=lo2.At)
-            _lora_dw(st, f"{path}.attn2.to_out.0", v_o2, sv["a2"], dh2, sv["u_o2"])
+            v_o2 = K.gemm(dh2, L.sBt_o2)
+            da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=L.At_o2)
+            dh2_t = _T(dh2)
+            _dw(g("attn2.A_o"), _T(v_o2), _T(sv["a2"]))
+            _dw(g("attn2.B_o"), dh2_t, _T(sv["u_o2"]), st.scale)
         else:
             da2 = K.gemm(dh2, o2.wt)
         enc = rt.enc
@@ -373,27 +427,30 @@ class BasicTransformerBlock(nn.Module):
                                     sv["lse2"], da2.view(B, S, C), a2m.heads, dk=dk3[..., :C], dv=dk3[..., C:])
         dq2 = dq2.view(M, C)
         if lo:
-            lq2, lk2, lv2 = L("attn2.to_q"), L("attn2.to_k"), L("attn2.to_v")
-            v_q2 = K.gemm(dq2, lq2.sBt)
-            dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=lq2.At)
-            _lora_dw(st, f"{path}.attn2.to_q", v_q2, sv["n2"], dq2, sv["u_q2"])
-            dk2, dv2 = dkv2[:, :C], dkv2[:, C:]
-            u_kv2 = sv["u_kv2"]
-            for nm, l, dd, uu in (("to_k", lk2, dk2, u_kv2[:, :r]), ("to_v", lv2, dv2, u_kv2[:, r:])):
-                vv = K.gemm(dd, l.sBt)
-                gA, gB = st.grad_views(f"{path}.attn2.{nm}")
-                K.gemm(_T(vv), rt.enc_t, out=gA, out_dtype=torch.float32, accumulate=True)
-                K.gemm(_T(dd), _T(uu), out=gB, out_dtype=torch.float32, accumulate=True, alpha=st.scale)
+            v_q2 = K.gemm(dq2, L.sBt_q2)
+            dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=L.At_q2)
+            _dw(g("attn2.A_q"), _T(v_q2), _T(sv["n2"]))
+            _dw(g("attn2.B_q"), _T(dq2), _T(sv["u_q2"]), st.scale)
+            # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
+            v_kv = torch.empty((B * Se, 2 * r), device=dh3.device, dtype=BF16)
+            K.gemm(dkv2[:, :C], L.sBt_kv2[:, :C], out=v_kv[:, :r])
+            K.gemm(dkv2[:, C:], L.sBt_kv2[:, C:], out=v_kv[:, r:])
+            _dw(g("attn2.A_kv"), _T(v_kv), rt.enc_t)
+            dkv_t = _T(dkv2)
+            u_t = _T(sv["u_kv2"])
+            gB = g("attn2.B_kv")
+            _dw(gB[:C], dkv_t[:C], u_t[:r], st.scale)
+            _dw(gB[C:], dkv_t[C:], u_t[r:], st.scale)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
         # --- self attention ---
         o1 = a1m.to_out[0]
         if lo:
-            lo1 = L("attn1.to_out.0")
-            v_o1 = K.gemm(dh1, lo1.sBt)
-            da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=lo1.At)
-            _lora_dw(st, f"{path}.attn1.to_out.0", v_o1, sv["a1"], dh1, sv["u_o1"])
+            v_o1 = K.gemm(dh1, L.sBt_o1)
+            da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=L.At_o1)
+            _dw(g("attn1.A_o"), _T(v_o1), _T(sv["a1"]))
+            _dw(g("attn1.B_o"), _T(dh1), _T(sv["u_o1"]), st.scale)
         else:
             da1 = K.gemm(dh1, o1.wt)
         q3 = sv["qkv"].view(B, S, 3 * C)
@@ -403,18 +460,15 @@ class BasicTransformerBlock(nn.Module):
                         da1.view(B, S, C), a1m.heads, dq=d3[..., :C], dk=d3[..., C:2 * C], dv=d3[..., 2 * C:])
         if lo:
             v_qkv = torch.empty((M, 3 * r), device=dh3.device, dtype=BF16)
-            names = ("to_q", "to_k", "to_v")
-            for j, nm in enumerate(names):
-                K.gemm(dqkv[:, j * C:(j + 1) * C], L(f"attn1.{nm}").sBt, out=v_qkv[:, j * r:(j + 1) * r])
-            dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=rt.lora_qkv_At[path])
-            n1t = _T(sv["n1"])
-            vt = _T(v_qkv)
-            ut = _T(sv["u_qkv"])
-            for j, nm in enumerate(names):
-                gA, gB = st.grad_views(f"{path}.attn1.{nm}")
-                K.gemm(vt[j * r:(j + 1) * r], n1t, out=gA, out_dtype=torch.float32, accumulate=True)
-                K.gemm(_T(dqkv[:, j * C:(j + 1) * C]), ut[j * r:(j + 1) * r], out=gB, out_dtype=torch.float32,
-                       accumulate=True, alpha=st.scale)
+            for j in range(3):
+                K.gemm(dqkv[:, j * C:(j + 1) * C], L.sBt_qkv[:, j * C:(j + 1) * C], out=v_qkv[:, j * r:(j + 1) * r])
+            dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv)
+            _dw(g("attn1.A_qkv"), _T(v_qkv), _T(sv["n1"]))
+            dqkv_t = _T(dqkv)
+            u_t = _T(sv["u_qkv"])
+            gB = g("attn1.B_qkv")
+            for j in range(3):
+                _dw(gB[j * C:(j + 1) * C], dqkv_t[j * C:(j + 1) * C], u_t[j * r:(j + 1) * r], st.scale)
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv)
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
@@ -665,7 +719,7 @@ class UNet2DConditionModel(nn.Module):
 
     def init_weights(self, seed=0):
         """PyTorch-default-style seeded init (the BASELINE synthetic-weights recipe); norms at identity."""
-        g = torch.Generator(device="cpu").manual_seed(seed)
+        g = torch.Generator(device=self.conv_in.weight.device).manual_seed(seed)
         for m in self.modules():
             if isinstance(m, (Linear, Conv2d, Norm)):
                 m.reset(g)
@@ -684,11 +738,9 @@ class UNet2DConditionModel(nn.Module):
         """peft LoraConfig(r, lora_alpha, init_lora_weights='gaussian', target_modules=[to_k,to_q,to_v,to_out.0])."""
         r = getattr(lora_config, "r", 32)
         alpha = getattr(lora_config, "lora_alpha", r)
-        entries = []
-        for name, blk in self._attn_modules():
-            entries += blk.lora_entries(name)
+        blocks = [(name, blk.dim, blk.attn2.kv_dim) for name, blk in self._attn_modules()]
         dev = self.conv_in.weight.device
-        self.lora = LoraState(entries, r, alpha, dev)
+        self.lora = LoraState(blocks, r, alpha, dev)
         if dev.type == "cuda":
             self.lora.init_gaussian(seed=getattr(lora_config, "seed", 0))
         self._adapters_enabled = True
@@ -724,27 +776,13 @@ class UNet2DConditionModel(nn.Module):
             self.refresh_lora()
 
     def refresh_lora(self):
-        st = self.lora
-        st.refresh()
-        r = st.r
-        self._lora_qkv_sB, self._lora_qkv_At, self._lora_kv_sB = {}, {}, {}
-        for name, blk in self._attn_modules():
-            c = st.cache
-            q, k, v = (c[f"{name}.attn1.{t}"] for t in ("to_q", "to_k", "to_v"))
-            self._lora_qkv_sB[name] = torch.cat([q.sB, k.sB, v.sB], 0)       # [3C][r]
-            self._lora_qkv_At[name] = torch.cat([q.At, k.At, v.At], 1)       # [C][3r]
-            k2, v2 = c[f"{name}.attn2.to_k"], c[f"{name}.attn2.to_v"]
-            self._lora_kv_sB[name] = torch.cat([k2.sB, v2.sB], 0)            # [2C][r]
+        self.lora.refresh()
 
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
         rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on)
-        if lora_on:
-            rt.lora = self.lora
-            rt.r = self.lora.r
-            rt.lora_qkv_sB, rt.lora_qkv_At, rt.lora_kv_sB = self._lora_qkv_sB, self._lora_qkv_At, self._lora_kv_sB
-        else:
-            rt.r = 0
+        rt.lora = self.lora
+        rt.r = self.lora.r if lora_on else 0
         return rt
 
     def _embed(self, timestep, time_ids, text_embeds, B, dev):

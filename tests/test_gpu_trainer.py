@@ -1,0 +1,100 @@
+"""End-to-end GPU parity of one PSO micro-step (tiny SDXL topology): loss and LoRA gradients of the HIP path vs the
+plain-torch fp32 reference of the whole micro-step (oracle UNet + the reference's turbo step / loss formulas)."""
+import math
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_turbo_lp(sample, eps, prev, sigma, s_up, dt):
+    """DP/turbo_inference_with_logprob.py:69-114 in torch (fp32), differentiable in eps."""
+    pred = sample - sigma * eps
+    deriv = (sample - pred) / sigma
+    mean = sample + deriv * dt
+    lp = -((prev - mean) ** 2) / (2 * s_up ** 2) - torch.log(s_up) - torch.log(torch.sqrt(2 * torch.as_tensor(math.pi)))
+    return lp.mean(dim=tuple(range(1, lp.ndim)))
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_micro_step_loss_and_grad_vs_fp32_reference(cuda, P):
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd import kernels as K
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+    unet.lora.init_gaussian(seed=1, b_std=0.05)
+    tr = PSOTrainer(unet, mode="turbo", num_steps=4, gradient_accumulation_steps=1, train_batch_size=P)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    enc = torch.randn(P, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(P, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(128, 0, cuda).repeat(P, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, 16, generator=g,
+                          reward_fn=lambda x: torch.rand(x.shape[0], device=cuda, generator=g))
+    assert torch.isfinite(buf["lp"]).all() and torch.isfinite(buf["x_final"]).all()
+    sb = tr.shuffle(buf, generator=g)
+    mb = tr.micro_batch(sb, 0)
+    st = unet.lora
+    st.grad.zero_()
+    tr.auto_step = False  # no optimizer step inside: inspect the accumulated grads
+    loss = tr.micro_step(mb)
+    mine_loss = loss.item()
+    mine_grads = {k: v.clone() for k, v in st.grad_dict_peft().items()}
+    # ---- fp32 reference of the same micro-step ----
+    sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
+    leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
+    ocfg = dict(time_proj_dim=cfg.time_proj_dim, addition_time_embed_dim=cfg.addition_time_embed_dim)
+    x_in = K.nhwc_to_nchw(mb.unet_in).float()
+    ep = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid, lora=leaf, cfg=ocfg)
+    with torch.no_grad():
+        er = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid, lora=None, cfg=ocfg)
+    # the reference casts UNet outputs to fp32 after a bf16 autocast forward: round eps to bf16 values
+    ep = ep + (ep.bfloat16().float() - ep).detach()
+    er = er.bfloat16().float()
+    xs = mb.x.permute(0, 3, 1, 2)
+    xp = mb.x_next.permute(0, 3, 1, 2)
+    c = mb.coef
+    sig, su, dt = (c[:, i].view(-1, 1, 1, 1) for i in (0, 1, 2))
+    lp_p = _ref_turbo_lp(xs, ep, xp, sig, su, dt)
+    lp_r = _ref_turbo_lp(xs, er, xp, sig, su, dt)
+    pref = K.preference(mb.rewards, 0)
+    d = (lp_p - lp_r).view(P, 2)
+    ratio = torch.clamp(torch.exp(d), 0.9, 1.1)
+    ref_loss = -torch.log(torch.sigmoid(50 * torch.log(ratio[:, 0]) * pref[:, 0] +
+                                        50 * torch.log(ratio[:, 1]) * pref[:, 1])).mean()
+    ref_loss.backward()
+    rel = abs(mine_loss - ref_loss.item()) / abs(ref_loss.item())
+    num = sum(((mine_grads[k] - v.grad) ** 2).sum().item() for k, v in leaf.items())
+    den = sum((v.grad ** 2).sum().item() for v in leaf.values())
+    grel = (num / max(den, 1e-30)) ** 0.5
+    print(f"P={P}: loss mine={mine_loss:.6f} ref={ref_loss.item():.6f} rel={rel:.2e}; grad rel={grel:.3e}")
+    # bf16 UNet activations vs the fp32 oracle: eps agree to ~1% (test_gpu_unet); beta=50 amplifies the resulting
+    # log-prob difference into the loss.  Loss-kernel parity on identical eps is 1e-5 (test_gpu_pso_loss).
+    assert rel < 1e-2
+    if den > 0:
+        assert grel < 1e-1
+
+
+def test_optimizer_step_matches_torch_adamw(cuda):
+    from pairwise_sample_optimization_amd import kernels as K
+    n = 10_000
+    g = torch.Generator(device="cuda").manual_seed(0)
+    p = torch.randn(n, device=cuda, generator=g)
+    grad = torch.randn(n, device=cuda, generator=g) * 3
+    p_ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([p_ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    for step in range(1, 4):
+        gg = grad * step
+        p_ref.grad = gg.clone()
+        torch.nn.utils.clip_grad_norm_([p_ref], 1.0)
+        opt.step()
+        clip = K.grad_clip_coef(gg, 1.0)
+        K.adamw_step(p, gg, m, v, 1e-3, (0.9, 0.999), 1e-8, 1e-2, step, clip=clip)
+    assert (p - p_ref.detach()).abs().max().item() < 1e-5

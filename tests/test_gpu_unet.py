@@ -58,10 +58,10 @@ def test_unet_forward_parity(cuda, which):
     assert e1 < 3e-2 and e0 < 3e-2
 
 
-@pytest.mark.parametrize("which", ["tiny16", "sdxl32"])
+@pytest.mark.parametrize("which", ["tiny16", "sdxl32", "sdxl64"])
 def test_unet_backward_lora_grad_parity(cuda, which):
     from pairwise_sample_optimization_amd.unet import UNetConfig
-    cfg = UNetConfig.tiny(16) if which == "tiny16" else UNetConfig.sdxl(32)
+    cfg = {"tiny16": UNetConfig.tiny(16), "sdxl32": UNetConfig.sdxl(32), "sdxl64": UNetConfig.sdxl(64)}[which]
     unet, sample, t, enc, text, tid = _setup(cuda, cfg)
     G = torch.randn(sample.shape, device=cuda, generator=torch.Generator(device="cuda").manual_seed(5))
     unet.lora.grad.zero_()
@@ -88,10 +88,30 @@ def test_unet_backward_lora_grad_parity(cuda, which):
 
 
 def _grad_dict(unet):
-    st = unet.lora
-    out = {}
-    for name in st.index:
-        gA, gB = st.views(st.grad, name)
-        out[f"{name}.lora_A.weight"] = gA
-        out[f"{name}.lora_B.weight"] = gB
-    return out
+    return unet.lora.grad_dict_peft()
+
+
+def test_unet_backward_bf16_torch_reference_noise(cuda):
+    """Diagnostic: how far does a bf16-autocast torch run of the same oracle (the reference's own numerics) land from
+    fp32 on the LoRA grads?  Printed next to the HIP path's error for the same tensors."""
+    from pairwise_sample_optimization_amd.unet import UNetConfig
+    cfg = UNetConfig.sdxl(32)
+    unet, sample, t, enc, text, tid = _setup(cuda, cfg)
+    G = torch.randn(sample.shape, device=cuda, generator=torch.Generator(device="cuda").manual_seed(5))
+    unet.lora.grad.zero_()
+    out = unet(sample, t, enc, added_cond_kwargs={"text_embeds": text, "time_ids": tid}).sample
+    (out * G).sum().backward()
+    mine = {k: v.clone() for k, v in _grad_dict(unet).items()}
+    leaf32 = {k: v.float().clone().requires_grad_(True) for k, v in unet.lora.state_dict_peft().items()}
+    (_oracle(unet, cfg, sample, t, enc, text, tid, True, lora_leaf=leaf32) * G).sum().backward()
+    leaf16 = {k: v.float().clone().requires_grad_(True) for k, v in unet.lora.state_dict_peft().items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        r16 = _oracle(unet, cfg, sample, t, enc, text, tid, True, lora_leaf=leaf16)
+    (r16.float() * G).sum().backward()
+    rows = sorted(((_rel(mine[k], v.grad), _rel(leaf16[k].grad, v.grad), k) for k, v in leaf32.items()),
+                  reverse=True)[:8]
+    tot = lambda d: (sum(((d[k] - v.grad) ** 2).sum().item() for k, v in leaf32.items()) /
+                     sum((v.grad ** 2).sum().item() for v in leaf32.values())) ** 0.5
+    print(f"\n total rel err vs fp32: hip={tot(mine):.3e} torch-bf16={tot({k: v.grad for k, v in leaf16.items()}):.3e}")
+    for a, b, k in rows:
+        print(f"   hip={a:.3e} torch-bf16={b:.3e}  {k}")

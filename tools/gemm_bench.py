@@ -1,0 +1,50 @@
+"""Micro-benchmark of the MFMA GEMM / implicit-GEMM conv kernel on the SDXL UNet's dominant shapes (1024^2, B=4)."""
+import sys
+import os
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pairwise_sample_optimization_amd import kernels as K  # noqa: E402
+
+
+def t_ms(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it
+
+
+def main():
+    dev = torch.device("cuda")
+    rows = []
+    for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (16384, 5120 * 2, 640, "L1 ff.proj"),
+                             (16384, 640, 2560, "L1 ff.out"), (16384, 1920, 640, "L1 qkv"),
+                             (16384, 640, 640, "L1 out/proj"), (4096, 10240 * 2, 1280, "L2 ff.proj"),
+                             (4096, 1280, 5120, "L2 ff.out"), (4096, 3840, 1280, "L2 qkv"),
+                             (4096, 1280, 1280, "L2 proj")]:
+        a = torch.randn(M, Kd, device=dev).bfloat16()
+        w = torch.randn(N, Kd, device=dev).bfloat16()
+        ms = t_ms(lambda: K.gemm(a, w))
+        rows.append((name, f"{M}x{N}x{Kd}", ms, 2 * M * N * Kd / ms / 1e9))
+    for (B, H, Ci, Co, name, mode) in [(4, 128, 320, 320, "L0 conv 320", K.CONV_NORMAL),
+                                       (4, 64, 640, 640, "L1 conv 640", K.CONV_NORMAL),
+                                       (4, 32, 1280, 1280, "L2 conv 1280", K.CONV_NORMAL),
+                                       (4, 32, 2560, 1280, "L2 conv 2560->1280", K.CONV_NORMAL),
+                                       (4, 64, 1280, 1280, "up conv 1280 @64->128", K.CONV_UP2)]:
+        x = torch.randn(B, H, H, Ci, device=dev).bfloat16()
+        w = torch.randn(Co, 3, 3, Ci, device=dev).bfloat16()
+        Ho = 2 * H if mode == K.CONV_UP2 else H
+        ms = t_ms(lambda: K.conv2d(x, w, mode=mode))
+        rows.append((name, f"B{B} {H}^2 {Ci}->{Co}", ms, 2 * B * Ho * Ho * Co * 9 * Ci / ms / 1e9))
+    for r in rows:
+        print(f"{r[0]:24s} {r[1]:22s} {r[2]:8.3f} ms  {r[3]:7.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
