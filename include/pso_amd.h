@@ -99,6 +99,12 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
              int tail_group_n, void* stream);
 
+/* TN GEMM, f32 accumulate: out[I][J] += alpha * sum_m A[m][I] * B[m][J] (A [M][I], B [M][J] row-major, row strides
+ * lda/ldb; I, J multiples of 8).  Replaces the peft LoRA weight-gradient GEMMs of the backward (dA = v^T x,
+ * dB = s dy^T u, reduction over tokens) without materialising transposes; split-K with f32 atomics. */
+int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                long ldo, void* stream);
+
 /* ------------------------------------------------------------------------------------------------------------------
  * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).
  * Input = channel concat of src1 [B][H][W][C1] and src2 [B][H][W][C2] (C2 may be 0); output [B][Ho][Wo][Cout] (ldo).
@@ -120,7 +126,7 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
  * GroupNorm (+ fused SiLU) on NHWC bf16, fp32 statistics.  stats [B][G][2] = (mean, rstd).
  * Replaces: torch.nn.GroupNorm(32) + SiLU of diffusers ResnetBlock2D (norm1/norm2), Transformer2DModel.norm,
  *           conv_norm_out (UNet, VAE decoder); its autograd backward (dx, optional dgamma/dbeta).
- * ws: pso_group_norm_ws_bytes(B,HW,C) for fwd; + B*G*2 floats for bwd.  dadd (optional) is added to dx.
+ * ws: pso_group_norm_ws_bytes(B,HW,C) bytes (fwd and bwd).  dadd (optional) is added to dx.
  * ---------------------------------------------------------------------------------------------------------------- */
 size_t pso_group_norm_ws_bytes(int B, int HW, int C);
 int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, const void* gamma, const void* beta,

@@ -38,6 +38,7 @@ SIGNATURES = {
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, vp]),
+    "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),
     "pso_group_norm_ws_bytes": (csz, [ci, ci, ci]),

@@ -66,36 +66,54 @@ __device__ __forceinline__ uint4 load_chunk_dense(const bf16_t* p, long ld, int 
   return make_uint4(0, 0, 0, 0);
 }
 
-__device__ __forceinline__ uint4 load_chunk_conv(const GemmArgs& g, const RowCoord& rc, int k) {
+// per-K-tile conv gather state (uniform over the tile: BK divides every channel source, so one tap / source)
+struct TapInfo {
+  int kh, kw;
+  int c0;            // channel offset inside the selected source
+  int Cs;            // channel count (row pitch) of the selected source
+  const bf16_t* src;
+  bool valid;
+};
+
+__device__ __forceinline__ TapInfo tap_info(const GemmArgs& g, int k0) {
   const ConvGeom& cv = g.conv;
   const int Ct = cv.C1 + cv.C2;
-  if (!rc.valid || k >= g.K1) return make_uint4(0, 0, 0, 0);
-  const int tap = k / Ct;
-  const int c = k - tap * Ct;
-  const int kh = tap / cv.ks, kw = tap - kh * cv.ks;
+  TapInfo t;
+  t.valid = k0 < g.K1;
+  const int tap = k0 / Ct;
+  const int c = k0 - tap * Ct;
+  t.kh = tap / cv.ks;
+  t.kw = tap - t.kh * cv.ks;
+  if (c < cv.C1) { t.src = g.a1; t.c0 = c; t.Cs = cv.C1; }
+  else { t.src = cv.src2; t.c0 = c - cv.C1; t.Cs = cv.C2; }
+  return t;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint4 load_chunk_conv(const ConvGeom& cv, const TapInfo& t, const RowCoord& rc, int kc) {
+  if (!rc.valid || !t.valid) return make_uint4(0, 0, 0, 0);
   int iy, ix;
-  if (cv.mode == PSO_CONV_NORMAL) {
-    iy = rc.oy * cv.stride + kh - cv.pad;
-    ix = rc.ox * cv.stride + kw - cv.pad;
-    if (iy < 0 || iy >= cv.H || ix < 0 || ix >= cv.W) return make_uint4(0, 0, 0, 0);
-  } else if (cv.mode == PSO_CONV_UP2) {
-    const int uy = rc.oy + kh - cv.pad, ux = rc.ox + kw - cv.pad;
-    if (uy < 0 || uy >= 2 * cv.H || ux < 0 || ux >= 2 * cv.W) return make_uint4(0, 0, 0, 0);
+  if (MODE == PSO_CONV_NORMAL) {
+    iy = rc.oy * cv.stride + t.kh - cv.pad;
+    ix = rc.ox * cv.stride + t.kw - cv.pad;
+    if ((unsigned)iy >= (unsigned)cv.H || (unsigned)ix >= (unsigned)cv.W) return make_uint4(0, 0, 0, 0);
+  } else if (MODE == PSO_CONV_UP2) {
+    const int uy = rc.oy + t.kh - cv.pad, ux = rc.ox + t.kw - cv.pad;
+    if ((unsigned)uy >= (unsigned)(2 * cv.H) || (unsigned)ux >= (unsigned)(2 * cv.W)) return make_uint4(0, 0, 0, 0);
     iy = uy >> 1;
     ix = ux >> 1;
   } else {  // T2
-    const int ty = rc.oy + cv.pad - kh, tx = rc.ox + cv.pad - kw;
+    const int ty = rc.oy + cv.pad - t.kh, tx = rc.ox + cv.pad - t.kw;
     if (ty < 0 || tx < 0 || (ty & 1) || (tx & 1)) return make_uint4(0, 0, 0, 0);
     iy = ty >> 1;
     ix = tx >> 1;
     if (iy >= cv.H || ix >= cv.W) return make_uint4(0, 0, 0, 0);
   }
   const long pix = ((long)rc.b * cv.H + iy) * cv.W + ix;
-  if (c < cv.C1) return *reinterpret_cast<const uint4*>(g.a1 + pix * cv.C1 + c);
-  return *reinterpret_cast<const uint4*>(cv.src2 + pix * cv.C2 + (c - cv.C1));
+  return *reinterpret_cast<const uint4*>(t.src + pix * t.Cs + t.c0 + kc);
 }
 
-template <int BM, int BN, bool CONV>
+template <int BM, int BN, int CONV>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) {
   using T = Tile<BM, BN>;
   constexpr int MI = BM / 32;  // 16-row subtiles per wave
@@ -119,7 +137,12 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
 
   const int nt1 = (g.K1 + BK - 1) / BK;
   const int nt2 = g.a2 ? (g.K2 + BK - 1) / BK : 0;
-  const int nt = nt1 + nt2;
+  const int nt_all = nt1 + nt2;
+  // split-K (gridDim.y > 1): this block owns K-tiles [t_beg, t_end); partials are added atomically (f32 out)
+  const int per = (nt_all + gridDim.y - 1) / gridDim.y;
+  const int t_beg = blockIdx.y * per;
+  const int t_end = min(nt_all, t_beg + per);
+  const int nt = t_end > t_beg ? t_end - t_beg : 0;
   const long a2_off = g.tail_group_n > 0 ? (long)(n0 / g.tail_group_n) * g.K2 : 0;
 
   // staging coordinates: chunk q = tid + 256*i -> row q/8, k-chunk q%8
@@ -139,15 +162,18 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
   }
   uint4 ra[T::A_CH], rb[T::B_CH];
 
-  auto load_tile = [&](int t) {
+  auto load_tile = [&](int tt) {
+    const int t = tt + t_beg;
     const bool second = t >= nt1;
     const int k0 = (second ? t - nt1 : t) * BK;
+    TapInfo ti;
+    if (CONV && !second) ti = tap_info(g, k0);
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
       const int q = tid + GEMM_THREADS * i;
       const int row = q >> 3, kc = (q & 7) * 8;
       if (second) ra[i] = load_chunk_dense(g.a2 + a2_off, g.lda2, m0 + row, g.M, k0 + kc, g.K2);
-      else if (CONV) ra[i] = load_chunk_conv(g, rc[i], k0 + kc);
+      else if (CONV) ra[i] = load_chunk_conv<CONV>(g.conv, ti, rc[i], kc);
       else ra[i] = load_chunk_dense(g.a1, g.lda1, m0 + row, g.M, k0 + kc, g.K1);
     }
 #pragma unroll
@@ -220,6 +246,11 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
       if (n >= g.N) continue;
       float v[4] = {acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
                     acc[i][j][3] * g.alpha};
+      if (gridDim.y > 1) {  // split-K partial: f32 accumulate output, no bias / residual (host-checked)
+        float* o = reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n;
+        for (int r = 0; r < 4 && n + r < g.N; ++r) atomicAdd(o + r, v[r]);
+        continue;
+      }
       const bool full = g.vec_ok && (n + 4 <= g.N);
       if (full) {
         if (g.bias) {
@@ -264,10 +295,15 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
 }
 
 template <int BM, int BN>
-static int launch(const GemmArgs& g, hipStream_t st) {
+static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  if (g.conv.mode) gemm_bf16_kernel<BM, BN, true><<<nblk, GEMM_THREADS, 0, st>>>(g);
-  else gemm_bf16_kernel<BM, BN, false><<<nblk, GEMM_THREADS, 0, st>>>(g);
+  dim3 grid(nblk, ksplit);
+  switch (g.conv.mode) {
+    case PSO_CONV_NORMAL: gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL><<<grid, GEMM_THREADS, 0, st>>>(g); break;
+    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2><<<grid, GEMM_THREADS, 0, st>>>(g); break;
+    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2><<<grid, GEMM_THREADS, 0, st>>>(g); break;
+    default: gemm_bf16_kernel<BM, BN, 0><<<grid, GEMM_THREADS, 0, st>>>(g);
+  }
   return pso_check_launch("pso_gemm");
 }
 
@@ -288,6 +324,120 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.N <= 64) return launch<128, 64>(g, st);
   if (g.M <= 64) return launch<64, 128>(g, st);
   return launch<128, 128>(g, st);
+}
+
+// =====================================================================================================================
+// TN GEMM: out[I][J] (+)= alpha * sum_m A[m][I] * B[m][J]   (both operands "token-major": the reduction index is the
+// row index).  This is the shape of every LoRA weight gradient (dA = v^T x, dB = s dy^T u, reduction over the
+// B*S tokens); it replaces two explicit transposes per product.  Tiles of 64 (m) rows x 64 columns are staged
+// row-major in LDS with the chunk ^ (2*((row>>1)&3)) swizzle and read as MFMA fragments with ds_read_b64_tr_b16
+// (lane i of a 16-lane group receives column i of 4 consecutive rows = 4 consecutive k of one output row).
+// Split-K over gridDim.y with f32 atomics in the epilogue (output is always an f32 accumulator).
+// =====================================================================================================================
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4_g;
+__device__ __forceinline__ int swz_tr64(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 3) << 1)) << 3); }
+
+__device__ __forceinline__ s16x4 tr_read64(const bf16_t* img, int r0, int col0, int lane) {
+  const int li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = col0 + 4 * p;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_g*)(img + swz_tr64(r0 + q, col >> 3) + (col & 7)));
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int M, int I, int J, const bf16_t* __restrict__ A, long lda,
+                                                         const bf16_t* __restrict__ B, long ldb, float alpha,
+                                                         float* __restrict__ out, long ldo) {
+  __shared__ __attribute__((aligned(16))) bf16_t sA[2][64 * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t sB[2][64 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int nbj = (J + 63) / 64;
+  const int bi = blockIdx.x / nbj, bj = blockIdx.x - bi * nbj;
+  const int i0 = bi * 64, j0 = bj * 64;
+  const int nkt = (M + 63) / 64;
+  const int per = (nkt + gridDim.y - 1) / gridDim.y;
+  const int t_beg = blockIdx.y * per, t_end = min(nkt, t_beg + per);
+  uint4 ra[2], rb[2];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = tid + 256 * h;
+      const int row = q >> 3, ch = q & 7;
+      const int m = t * 64 + row;
+      const int ci = i0 + ch * 8, cj = j0 + ch * 8;
+      ra[h] = (m < M && ci < I) ? *reinterpret_cast<const uint4*>(A + (long)m * lda + ci) : make_uint4(0, 0, 0, 0);
+      rb[h] = (m < M && cj < J) ? *reinterpret_cast<const uint4*>(B + (long)m * ldb + cj) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = tid + 256 * h;
+      const int row = q >> 3, ch = q & 7;
+      *reinterpret_cast<uint4*>(sA[buf] + swz_tr64(row, ch)) = ra[h];
+      *reinterpret_cast<uint4*>(sB[buf] + swz_tr64(row, ch)) = rb[h];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, c = lane & 15;
+  if (t_beg < t_end) {
+    load(t_beg);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = t_beg; t < t_end; ++t) {
+    const int cur = (t - t_beg) & 1;
+    if (t + 1 < t_end) load(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int col = wi * 32 + a * 16;
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        const s16x4 x0 = tr_read64(sA[cur], ks * 32 + 8 * g, col, lane);
+        const s16x4 x1 = tr_read64(sA[cur], ks * 32 + 8 * g + 4, col, lane);
+        s16x8 v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        af[a] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int col = wj * 32 + b * 16;
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        const s16x4 y0 = tr_read64(sB[cur], ks * 32 + 8 * g, col, lane);
+        const s16x4 y1 = tr_read64(sB[cur], ks * 32 + 8 * g + 4, col, lane);
+        s16x8 v = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+        bfr[b] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    if (t + 1 < t_end) store(cur ^ 1);
+    __syncthreads();
+  }
+  // lane holds out[i = i0 + wi*32 + a*16 + c][j = j0 + wj*32 + b*16 + 4g + r]
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int i = i0 + wi * 32 + a * 16 + c;
+    if (i >= I) continue;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int j = j0 + wj * 32 + b * 16 + 4 * g;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (j + r < J) {
+          float* o = out + (long)i * ldo + j + r;
+          if (gridDim.y > 1) atomicAdd(o, acc[a][b][r] * alpha);
+          else *o += acc[a][b][r] * alpha;
+        }
+    }
+  }
 }
 
 extern "C" {
@@ -347,6 +497,22 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
   return run_gemm(g, (hipStream_t)stream);
+}
+
+int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                long ldo, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && I > 0 && J > 0 && A && B && out, "pso_gemm_tn: bad args");
+  PSO_ARG_CHECK(al16(A) && al16(B) && (lda % 8) == 0 && (ldb % 8) == 0 && (I % 8) == 0 && (J % 8) == 0,
+                "pso_gemm_tn: operands need 16-B aligned rows and I, J multiples of 8");
+  if (M == 0) return PSO_OK;
+  const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
+  const int nkt = (M + 63) / 64;
+  int ks = (512 + tiles - 1) / tiles;
+  if (ks > nkt) ks = nkt;
+  if (ks < 1) ks = 1;
+  gemm_tn_kernel<<<dim3(tiles, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B,
+                                                                   ldb, alpha, out, ldo);
+  return pso_check_launch("pso_gemm_tn");
 }
 
 }  // extern "C"

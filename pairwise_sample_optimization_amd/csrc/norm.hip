@@ -30,12 +30,15 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------------------------------------------
-// partial sums.  BWD=false: (x) -> sum x, sum x^2.  BWD=true: (x, dy, stats, gamma, beta) -> sum dz, sum dz*xhat
+// partial sums.  BWD=false: (x) -> per group sum x, sum x^2.
+//                BWD=true:  (x, dy, stats, gamma, beta) -> per group sum dz*gamma, sum dz*gamma*xhat
+//                           (+ optional per-channel sum dz, sum dz*xhat for dbeta / dgamma)
+// ws layout: [B][chunks][G][2] (+ per-channel [B][chunks][C][2] after it when DPARAM)
 // ---------------------------------------------------------------------------------------------------------------
 template <bool BWD, bool SILU>
 __global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                   const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
-                                  const bf16_t* __restrict__ beta, float* __restrict__ ws) {
+                                  const bf16_t* __restrict__ beta, float* __restrict__ ws, float* __restrict__ ws_ch) {
   extern __shared__ float red[];  // [RS][C][2]
   const int TPR = C / 8;
   const int RS = blockDim.x / TPR;
@@ -86,7 +89,6 @@ __global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict
       }
     }
   }
-  // reduce over slots through LDS
   if (slot < RS) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -95,35 +97,58 @@ __global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict
     }
   }
   __syncthreads();
+  // fold the row slots: per-channel sums back into slot 0
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float a = 0.f, q = 0.f;
     for (int s = 0; s < RS; ++s) {
       a += red[(s * C + c) * 2];
       q += red[(s * C + c) * 2 + 1];
     }
-    float* o = ws + (((size_t)b * nchunks + chunk) * C + c) * 2;
+    if (ws_ch) {
+      float* o = ws_ch + (((size_t)b * nchunks + chunk) * C + c) * 2;
+      o[0] = a;
+      o[1] = q;
+    }
+    if (BWD && gamma) {  // the group coefficients need gamma-weighted sums
+      const float gmc = bf2f(gamma[c]);
+      a *= gmc;
+      q *= gmc;
+    }
+    red[c * 2] = a;
+    red[c * 2 + 1] = q;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    float a = 0.f, q = 0.f;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      a += red[c * 2];
+      q += red[c * 2 + 1];
+    }
+    float* o = ws + (((size_t)b * nchunks + chunk) * G + g) * 2;
     o[0] = a;
     o[1] = q;
   }
 }
 
-// one thread per (image, group).  FWD: stats = (mean, rstd).  BWD: coef = (mean(dz*gamma), mean(dz*gamma*xhat)).
+// one wave per (image, group): fixed-order fp64 combine over the chunks.
+// FWD: stats = (mean, rstd).  BWD: coef = (mean(dz*gamma), mean(dz*gamma*xhat)).
 template <bool BWD>
 __global__ void gn_finalize_kernel(int B, int HW, int C, int G, int nchunks, float eps, const float* __restrict__ ws,
-                                   const bf16_t* __restrict__ gamma, float* __restrict__ out) {
-  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+                                   float* __restrict__ out) {
+  const int id = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (id >= B * G) return;
   const int b = id / G, g = id - b * G;
   const int Cg = C / G;
   double a = 0.0, q = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
-    const float* p = ws + (((size_t)b * nchunks + k) * C + g * Cg) * 2;
-    for (int c = 0; c < Cg; ++c) {
-      const double gm = BWD ? (gamma ? (double)bf2f(gamma[g * Cg + c]) : 1.0) : 1.0;
-      a += gm * p[2 * c];
-      q += gm * p[2 * c + 1];
-    }
+  for (int k = lane; k < nchunks; k += 64) {
+    const float* p = ws + (((size_t)b * nchunks + k) * G + g) * 2;
+    a += p[0];
+    q += p[1];
   }
+  a = warp_sum_d(a);
+  q = warp_sum_d(q);
+  if (lane != 0) return;
   const double n = (double)HW * Cg;
   if (!BWD) {
     const double mean = a / n;
@@ -137,7 +162,7 @@ __global__ void gn_finalize_kernel(int B, int HW, int C, int G, int nchunks, flo
   }
 }
 
-// per-channel dgamma/dbeta from the bwd partials (sum over images and chunks)
+// per-channel dgamma/dbeta from the per-channel bwd partials (sum over images and chunks)
 __global__ void gn_dparam_kernel(int B, int C, int nchunks, const float* __restrict__ ws, float* __restrict__ dgamma,
                                  float* __restrict__ dbeta, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -326,7 +351,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int C, const bf16_t*
 extern "C" {
 
 size_t pso_group_norm_ws_bytes(int B, int HW, int C) {
-  return (size_t)B * cdiv(HW, GN_ROWS) * C * 2 * sizeof(float);
+  // group partials (G <= C) + per-channel partials (dgamma/dbeta) + group coefficients
+  return (size_t)B * cdiv(HW, GN_ROWS) * C * 2 * sizeof(float) * 2 + (size_t)B * C * 2 * sizeof(float);
 }
 
 int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, const void* gamma, const void* beta,
@@ -340,9 +366,9 @@ int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, co
   const int threads = gn_block(C);
   const size_t shm = (size_t)(threads / (C / 8)) * C * 2 * sizeof(float);
   gn_partial_kernel<false, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, (const bf16_t*)x, nullptr,
-                                                                          nullptr, nullptr, nullptr, (float*)ws);
-  gn_finalize_kernel<false><<<cdiv(B * G, 128), 128, 0, st>>>(B, HW, C, G, nchunks, eps, (const float*)ws, nullptr,
-                                                              stats);
+                                                                          nullptr, nullptr, nullptr, (float*)ws,
+                                                                          nullptr);
+  gn_finalize_kernel<false><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, eps, (const float*)ws, stats);
   const long nvec = (long)B * HW * C / 8;
   if (silu)
     gn_apply_fwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, (const bf16_t*)x, stats,
@@ -359,23 +385,26 @@ int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* d
   PSO_ARG_CHECK(B > 0 && HW > 0 && C > 0 && G > 0 && C % G == 0 && C % 8 == 0 && C <= 4096,
                 "pso_group_norm_bwd: bad shape");
   PSO_ARG_CHECK(x && dy && stats && dx && ws, "pso_group_norm_bwd: null pointer");
-  PSO_ARG_CHECK(ws_bytes >= pso_group_norm_ws_bytes(B, HW, C) + (size_t)B * G * 2 * sizeof(float),
-                "pso_group_norm_bwd: workspace too small");
+  PSO_ARG_CHECK(ws_bytes >= pso_group_norm_ws_bytes(B, HW, C), "pso_group_norm_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const int nchunks = cdiv(HW, GN_ROWS);
   const int threads = gn_block(C);
   const size_t shm = (size_t)(threads / (C / 8)) * C * 2 * sizeof(float);
-  float* part = (float*)ws;
-  float* coef = (float*)((char*)ws + pso_group_norm_ws_bytes(B, HW, C));
+  const size_t half = (size_t)B * nchunks * C * 2;
+  float* part = (float*)ws;                       // [B][chunks][G][2]
+  float* part_ch = (dgamma || dbeta) ? part + half : nullptr;  // [B][chunks][C][2]
+  float* coef = part + 2 * half;                  // [B][G][2]
   const bf16_t *xp = (const bf16_t*)x, *dyp = (const bf16_t*)dy, *gp = (const bf16_t*)gamma,
                *bp = (const bf16_t*)beta;
   if (silu)
-    gn_partial_kernel<true, true><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part);
+    gn_partial_kernel<true, true><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part,
+                                                                          part_ch);
   else
-    gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part);
-  gn_finalize_kernel<true><<<cdiv(B * G, 128), 128, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, gp, coef);
+    gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part,
+                                                                           part_ch);
+  gn_finalize_kernel<true><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, coef);
   if (dgamma || dbeta)
-    gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part, dgamma, dbeta, accumulate_dparams);
+    gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part_ch, dgamma, dbeta, accumulate_dparams);
   const long nvec = (long)B * HW * C / 8;
   if (silu)
     gn_apply_bwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, xp, dyp, stats, coef, gp, bp,

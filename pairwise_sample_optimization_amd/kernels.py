@@ -63,6 +63,18 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
     return out
 
 
+def gemm_tn(a, b, out, alpha=1.0):
+    """out[I,J] (f32, accumulated) += alpha * a^T @ b  with a [M,I], b [M,J] (row-strided views)."""
+    M, I = a.shape
+    J = b.shape[1]
+    assert b.shape[0] == M and out.shape == (I, J) and out.dtype == torch.float32
+    e0 = _prof_begin()
+    check(lib().pso_gemm_tn(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
+                            _row_stride(out), stream_ptr()), "pso_gemm_tn")
+    _prof_end(e0, 2.0 * M * I * J)
+    return out
+
+
 def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=None, bias=None, rowbias=None,
            resid=None, a2=None, w2=None, alpha=1.0, out=None, out_dtype=BF16, accumulate=False):
     """NHWC implicit-GEMM conv.  x [B,H,W,C1] (+ x2 [B,H,W,C2] concatenated on channels); weight [Cout,ks,ks,C1+C2].
@@ -168,7 +180,7 @@ def group_norm_bwd(x, dy, stats, gamma, beta, silu, dadd=None, dgamma=None, dbet
     G = stats.shape[1]
     HW = x.numel() // (B * C)
     dx = torch.empty_like(x)
-    wsb = lib().pso_group_norm_ws_bytes(B, HW, C) + B * G * 2 * 4
+    wsb = lib().pso_group_norm_ws_bytes(B, HW, C)
     ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
     check(lib().pso_group_norm_bwd(B, HW, C, G, ptr(x), ptr(dy.contiguous()), ptr(stats), ptr(gamma), ptr(beta),
                                    int(silu), ptr(dadd), ptr(dx), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(ws),

@@ -285,16 +285,6 @@ class LoraState:
         self.refresh()
 
 
-def _T(x, pad_to=8):
-    """[M][C] -> [C][Mp] with the reduction dim zero-padded to a multiple of `pad_to` (GEMM K % 8 == 0)."""
-    return K.transpose(x, pad_rows_to=pad_to)
-
-
-def _dw(out, a_t, b_t, alpha=1.0):
-    """out[f32] += alpha * a_t . b_t^T  with both operands already transposed ([rows][Mp], [cols][Mp])."""
-    K.gemm(a_t, b_t, out=out, out_dtype=torch.float32, accumulate=True, alpha=alpha)
-
-
 # ======================================================================================================================
 # blocks: fwd(x, rt) -> y (saving what bwd needs in a dict when rt.save) ; bwd(dy, saved, rt) -> dx
 # ======================================================================================================================
@@ -413,9 +403,8 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_o2 = K.gemm(dh2, L.sBt_o2)
             da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=L.At_o2)
-            dh2_t = _T(dh2)
-            _dw(g("attn2.A_o"), _T(v_o2), _T(sv["a2"]))
-            _dw(g("attn2.B_o"), dh2_t, _T(sv["u_o2"]), st.scale)
+            K.gemm_tn(v_o2, sv["a2"], g("attn2.A_o"))
+            K.gemm_tn(dh2, sv["u_o2"], g("attn2.B_o"), st.scale)
         else:
             da2 = K.gemm(dh2, o2.wt)
         enc = rt.enc
@@ -429,18 +418,17 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_q2 = K.gemm(dq2, L.sBt_q2)
             dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=L.At_q2)
-            _dw(g("attn2.A_q"), _T(v_q2), _T(sv["n2"]))
-            _dw(g("attn2.B_q"), _T(dq2), _T(sv["u_q2"]), st.scale)
+            K.gemm_tn(v_q2, sv["n2"], g("attn2.A_q"))
+            K.gemm_tn(dq2, sv["u_q2"], g("attn2.B_q"), st.scale)
             # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
             v_kv = torch.empty((B * Se, 2 * r), device=dh3.device, dtype=BF16)
             K.gemm(dkv2[:, :C], L.sBt_kv2[:, :C], out=v_kv[:, :r])
             K.gemm(dkv2[:, C:], L.sBt_kv2[:, C:], out=v_kv[:, r:])
-            _dw(g("attn2.A_kv"), _T(v_kv), rt.enc_t)
-            dkv_t = _T(dkv2)
-            u_t = _T(sv["u_kv2"])
+            K.gemm_tn(v_kv, rt.enc, g("attn2.A_kv"))
             gB = g("attn2.B_kv")
-            _dw(gB[:C], dkv_t[:C], u_t[:r], st.scale)
-            _dw(gB[C:], dkv_t[C:], u_t[r:], st.scale)
+            u_kv2 = sv["u_kv2"]
+            K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
+            K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
@@ -449,8 +437,8 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_o1 = K.gemm(dh1, L.sBt_o1)
             da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=L.At_o1)
-            _dw(g("attn1.A_o"), _T(v_o1), _T(sv["a1"]))
-            _dw(g("attn1.B_o"), _T(dh1), _T(sv["u_o1"]), st.scale)
+            K.gemm_tn(v_o1, sv["a1"], g("attn1.A_o"))
+            K.gemm_tn(dh1, sv["u_o1"], g("attn1.B_o"), st.scale)
         else:
             da1 = K.gemm(dh1, o1.wt)
         q3 = sv["qkv"].view(B, S, 3 * C)
@@ -463,12 +451,11 @@ class BasicTransformerBlock(nn.Module):
             for j in range(3):
                 K.gemm(dqkv[:, j * C:(j + 1) * C], L.sBt_qkv[:, j * C:(j + 1) * C], out=v_qkv[:, j * r:(j + 1) * r])
             dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv)
-            _dw(g("attn1.A_qkv"), _T(v_qkv), _T(sv["n1"]))
-            dqkv_t = _T(dqkv)
-            u_t = _T(sv["u_qkv"])
+            K.gemm_tn(v_qkv, sv["n1"], g("attn1.A_qkv"))
             gB = g("attn1.B_qkv")
+            u_qkv = sv["u_qkv"]
             for j in range(3):
-                _dw(gB[j * C:(j + 1) * C], dqkv_t[j * C:(j + 1) * C], u_t[j * r:(j + 1) * r], st.scale)
+                K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C], st.scale)
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv)
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
@@ -807,8 +794,6 @@ class UNet2DConditionModel(nn.Module):
         lora_on = self.lora is not None and self._adapters_enabled
         encf = enc.to(BF16).reshape(B * enc.shape[1], enc.shape[2]).contiguous()
         rt = self._runtime(B, encf, save, lora_on)
-        if save and lora_on:
-            rt.enc_t = _T(encf)
         temb_all = self._embed(timestep, time_ids, text_embeds, B, x.device)
         tb = lambda m: temb_all[:, m._temb_off:m._temb_off + m.cout]
         # conv_in (C=4): im2col GEMM

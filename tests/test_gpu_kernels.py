@@ -106,3 +106,26 @@ def test_conv_stride1_input_grad_flipped(cuda):
     wf = w.flip(2, 3).permute(1, 2, 3, 0).contiguous().bfloat16()  # [Ci][kh'][kw'][Co]
     out = K_.conv2d(_nhwc(dy.bfloat16()), wf, out_dtype=torch.float32)
     assert _rel(_nchw(out), gx) < 1e-5
+
+
+@pytest.mark.parametrize("M,I,J", [(16384, 96, 640), (308, 32, 2048), (4096, 1280, 32), (100, 64, 8)])
+def test_gemm_tn_vs_fp32(cuda, M, I, J):
+    from pairwise_sample_optimization_amd import kernels as K_
+    big = torch.randn(M, I + 16, device=cuda).bfloat16()
+    a = big[:, 8:8 + I]          # column-slice view (row stride != I)
+    b = torch.randn(M, J, device=cuda).bfloat16()
+    out = torch.randn(I, J, device=cuda)
+    ref = out + 0.5 * (a.float().t() @ b.float())
+    K_.gemm_tn(a, b, out, alpha=0.5)
+    assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 640, 16384), (1280, 32, 4096), (96, 1280, 8192)])
+def test_gemm_splitk_accumulate(cuda, M, N, K):
+    from pairwise_sample_optimization_amd import kernels as K_
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    out = torch.randn(M, N, device=cuda)
+    ref = out + a.float() @ w.float().t()
+    K_.gemm(a, w, out=out, out_dtype=torch.float32, accumulate=True)
+    assert _rel(out, ref) < 1e-5

