@@ -99,6 +99,10 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
              int tail_group_n, void* stream);
 
+/* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
+ * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage). */
+void pso_gemm_set_variant(int v);
+
 /* TN GEMM, f32 accumulate: out[I][J] += alpha * sum_m A[m][I] * B[m][J] (A [M][I], B [M][J] row-major, row strides
  * lda/ldb; I, J multiples of 8).  Replaces the peft LoRA weight-gradient GEMMs of the backward (dA = v^T x,
  * dB = s dy^T u, reduction over tokens) without materialising transposes; split-K with f32 atomics. */
@@ -190,7 +194,11 @@ int pso_transpose_batched(int n, const void* descs, int max_r, int max_c, void* 
 /* dst row i = src row idx[i] (row_bytes % 4 == 0): the pair/time shuffles of the trajectory buffer (T:733-745) */
 int pso_gather_rows(long n, long row_bytes, const void* src, const int64_t* idx, void* dst, void* stream);
 /* layout conversion of the (small) latent tensors at the diffusers NCHW API boundary */
-int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream);
+int pso_nchw_to_nhwc(int B, int C, int Cp, long HW, const void* src, int src_dtype, float scale, void* dst,
+                     void* stream);  /* channels zero-padded to Cp, values scaled */
+/* in-place row softmax of a bf16 [M][N] score matrix (fp32 math): the single-head 16384-token attention of the SDXL
+ * VAE decoder mid-block (diffusers Attention, head dim 512) runs as GEMM -> softmax -> GEMM */
+int pso_softmax_rows(int M, int N, void* x, long ld, void* stream);
 int pso_nhwc_to_nchw(int B, int C, long HW, const void* src, void* dst, int dst_dtype, void* stream);
 int pso_concat_channels(long npix, int C1, const void* x1, int C2, const void* x2, void* out, void* stream);
 int pso_split_channels(long npix, int C1, int C2, const void* in, void* y1, void* y2, const void* add2,

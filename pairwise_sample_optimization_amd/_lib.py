@@ -38,6 +38,7 @@ SIGNATURES = {
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, vp]),
+    "pso_gemm_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),
@@ -62,7 +63,8 @@ SIGNATURES = {
     "pso_cast_bf16_f32": (ci, [cl, vp, vp, vp]),
     "pso_conv_weight_t": (ci, [ci, ci, ci, ci, vp, vp, vp]),
     "pso_concat_channels": (ci, [cl, ci, vp, ci, vp, vp, vp]),
-    "pso_nchw_to_nhwc": (ci, [ci, ci, cl, vp, ci, vp, vp]),
+    "pso_nchw_to_nhwc": (ci, [ci, ci, ci, cl, vp, ci, cf, vp, vp]),
+    "pso_softmax_rows": (ci, [ci, ci, vp, cl, vp]),
     "pso_grad_clip_ws_bytes": (csz, [cl]),
     "pso_transpose_batched": (ci, [ci, vp, ci, ci, vp]),
     "pso_gather_rows": (ci, [cl, cl, vp, vp, vp, vp]),

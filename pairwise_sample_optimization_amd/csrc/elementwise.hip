@@ -241,14 +241,16 @@ __global__ void split_kernel(long npix, int C1, int C2, const bf16_t* __restrict
 }
 
 // NCHW (fp32 or bf16) -> NHWC bf16, and back (fp32 or bf16 out).  Small tensors (latents): plain element mapping.
-__global__ void nchw_to_nhwc_kernel(int B, int C, long HW, const void* __restrict__ src, int src_f32,
-                                    bf16_t* __restrict__ dst) {
-  GRID_STRIDE(i, (long)B * C * HW) {
-    const int c = (int)(i % C);
-    const long p = (i / C) % HW;
-    const int b = (int)(i / (C * HW));
+__global__ void nchw_to_nhwc_kernel(int B, int C, int Cp, long HW, const void* __restrict__ src, int src_f32,
+                                    float scale, bf16_t* __restrict__ dst) {
+  GRID_STRIDE(i, (long)B * Cp * HW) {
+    const int c = (int)(i % Cp);
+    const long p = (i / Cp) % HW;
+    const int b = (int)(i / (Cp * HW));
     const long s = ((long)b * C + c) * HW + p;
-    dst[i] = src_f32 ? f2bf(reinterpret_cast<const float*>(src)[s]) : reinterpret_cast<const bf16_t*>(src)[s];
+    float v = 0.f;
+    if (c < C) v = src_f32 ? reinterpret_cast<const float*>(src)[s] : bf2f(reinterpret_cast<const bf16_t*>(src)[s]);
+    dst[i] = f2bf(v * scale);
   }
 }
 __global__ void nhwc_to_nchw_kernel(int B, int C, long HW, const bf16_t* __restrict__ src, void* __restrict__ dst,
@@ -297,7 +299,49 @@ __global__ void gather_rows_kernel(long n, long units, const U* __restrict__ src
   }
 }
 
+// in-place row softmax of bf16 scores (fp32 math): one 256-thread block per row, 3 passes over the (L2-resident) row
+__global__ __launch_bounds__(256) void softmax_rows_kernel(int N, bf16_t* __restrict__ x, long ld) {
+  __shared__ float red[4];
+  bf16_t* row = x + blockIdx.x * ld;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float a[8];
+    unpack8e(*reinterpret_cast<const uint4*>(row + c), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, a[j]);
+  }
+  mx = warp_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float a[8];
+    unpack8e(*reinterpret_cast<const uint4*>(row + c), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(a[j] - mx);
+  }
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float a[8];
+    unpack8e(*reinterpret_cast<const uint4*>(row + c), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = __expf(a[j] - mx) * inv;
+    *reinterpret_cast<uint4*>(row + c) = pack8e(a);
+  }
+}
+
 extern "C" {
+
+int pso_softmax_rows(int M, int N, void* x, long ld, void* stream) {
+  PSO_ARG_CHECK(N % 8 == 0 && ld % 8 == 0 && x, "pso_softmax_rows: N, ld multiples of 8");
+  softmax_rows_kernel<<<M, 256, 0, (hipStream_t)stream>>>(N, (bf16_t*)x, ld);
+  return pso_check_launch("pso_softmax_rows");
+}
 
 int pso_transpose_batched(int n, const void* descs, int max_r, int max_c, void* stream) {
   PSO_ARG_CHECK(n > 0 && descs, "pso_transpose_batched: bad args");
@@ -317,10 +361,11 @@ int pso_gather_rows(long n, long row_bytes, const void* src, const int64_t* idx,
   return pso_check_launch("pso_gather_rows");
 }
 
-int pso_nchw_to_nhwc(int B, int C, long HW, const void* src, int src_dtype, void* dst, void* stream) {
-  PSO_ARG_CHECK(src && dst && (src_dtype == PSO_F32 || src_dtype == PSO_BF16), "pso_nchw_to_nhwc: bad args");
-  nchw_to_nhwc_kernel<<<grid_for((long)B * C * HW), 256, 0, (hipStream_t)stream>>>(B, C, HW, src,
-                                                                                  src_dtype == PSO_F32, (bf16_t*)dst);
+int pso_nchw_to_nhwc(int B, int C, int Cp, long HW, const void* src, int src_dtype, float scale, void* dst,
+                     void* stream) {
+  PSO_ARG_CHECK(src && dst && Cp >= C && (src_dtype == PSO_F32 || src_dtype == PSO_BF16), "pso_nchw_to_nhwc: bad args");
+  nchw_to_nhwc_kernel<<<grid_for((long)B * Cp * HW), 256, 0, (hipStream_t)stream>>>(
+      B, C, Cp, HW, src, src_dtype == PSO_F32, scale, (bf16_t*)dst);
   return pso_check_launch("pso_nchw_to_nhwc");
 }
 

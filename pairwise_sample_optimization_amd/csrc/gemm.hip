@@ -49,10 +49,10 @@ struct GemmArgs {
 
 __device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ (r & 7)) << 3); }
 
-template <int BM, int BN>
+template <int BM, int BN, int WAVES>
 struct Tile {
-  static constexpr int A_CH = BM * BK / 8 / GEMM_THREADS;  // 16-B chunks per thread
-  static constexpr int B_CH = BN * BK / 8 / GEMM_THREADS;
+  static constexpr int A_CH = BM / 8 / WAVES;  // 8-row x 128-B glds pieces per wave per K-tile
+  static constexpr int B_CH = BN / 8 / WAVES;
 };
 
 // ---- per-row conv coordinates (precomputed once per thread) ----
@@ -113,16 +113,30 @@ __device__ __forceinline__ uint4 load_chunk_conv(const ConvGeom& cv, const TapIn
   return *reinterpret_cast<const uint4*>(t.src + pix * t.Cs + t.c0 + kc);
 }
 
-template <int BM, int BN, int CONV>
-__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) {
-  using T = Tile<BM, BN>;
-  constexpr int MI = BM / 32;  // 16-row subtiles per wave
-  constexpr int NJ = BN / 32;  // 16-col subtiles per wave
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][(BM + BN) * BK];
+__device__ __attribute__((aligned(16))) uint4 g_zero16[4];  // source of every zero-filled (padding / tail) chunk
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Direct-to-LDS staging (global_load_lds_dwordx4): wave w fills 8-row x 128-B pieces; lane i of a piece lands at
+// byte 16*i of it (row i/8, physical chunk i%8), so the XOR swizzle is applied to the SOURCE chunk: physical chunk p of
+// row R holds logical chunk p ^ (R & 7) -- the same involution swz() applies on the read side.
+// WM x WN waves, each owning a (BM/WM) x (BN/WN) accumulator tile; STAGES-deep LDS ring with STAGES-1 K-tiles of
+// direct-to-LDS loads in flight behind a counted vmcnt and a raw s_barrier (a __syncthreads() would drain them).
+template <int BM, int BN, int CONV, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int WAVES = WM * WN;
+  using T = Tile<BM, BN, WAVES>;
+  constexpr int MI = BM / WM / 16;  // 16-row subtiles per wave
+  constexpr int NJ = BN / WN / 16;  // 16-col subtiles per wave
+  constexpr int PIECES = T::A_CH + T::B_CH;  // glds per wave per K-tile
+  static_assert(T::A_CH * WAVES * 8 == BM && T::B_CH * WAVES * 8 == BN, "tile / wave split");
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds_dyn[];
+  bf16_t* lds_base = lds_dyn;
+  auto stage_ptr = [&](int s) { return lds_base + s * (BM + BN) * BK; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
 
   // XCD-aware block order: blocks b, b+8, b+16 ... share an XCD; give each XCD a contiguous run of tiles.
   const int nbn = (g.N + BN - 1) / BN, nbm = (g.M + BM - 1) / BM;
@@ -145,12 +159,15 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
   const int nt = t_end > t_beg ? t_end - t_beg : 0;
   const long a2_off = g.tail_group_n > 0 ? (long)(n0 / g.tail_group_n) * g.K2 : 0;
 
-  // staging coordinates: chunk q = tid + 256*i -> row q/8, k-chunk q%8
+  // this lane's staging rows: piece j of wave w covers rows (w*PIECES + j)*8 .. +8
+  const int prow = lane >> 3;
+  const int pch = lane & 7;
   RowCoord rc[T::A_CH];
   if (CONV) {
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
-      const int m = m0 + (tid + GEMM_THREADS * i) / 8;
+      const int R = (wave * T::A_CH + i) * 8 + prow;
+      const int m = m0 + R;
       const int hw = g.conv.Ho * g.conv.Wo;
       rc[i].valid = m < g.M;
       const int mm = rc[i].valid ? m : 0;
@@ -160,42 +177,66 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
       rc[i].ox = rem - rc[i].oy * g.conv.Wo;
     }
   }
-  uint4 ra[T::A_CH], rb[T::B_CH];
+  const uint4* zero = g_zero16;
 
-  auto load_tile = [&](int tt) {
+  auto issue_tile = [&](int tt, int buf) {
     const int t = tt + t_beg;
     const bool second = t >= nt1;
     const int k0 = (second ? t - nt1 : t) * BK;
     TapInfo ti;
     if (CONV && !second) ti = tap_info(g, k0);
+    bf16_t* la = stage_ptr(buf);
+    bf16_t* lb = stage_ptr(buf) + BM * BK;
 #pragma unroll
     for (int i = 0; i < T::A_CH; ++i) {
-      const int q = tid + GEMM_THREADS * i;
-      const int row = q >> 3, kc = (q & 7) * 8;
-      if (second) ra[i] = load_chunk_dense(g.a2 + a2_off, g.lda2, m0 + row, g.M, k0 + kc, g.K2);
-      else if (CONV) ra[i] = load_chunk_conv<CONV>(g.conv, ti, rc[i], kc);
-      else ra[i] = load_chunk_dense(g.a1, g.lda1, m0 + row, g.M, k0 + kc, g.K1);
+      const int piece = wave * T::A_CH + i;
+      const int R = piece * 8 + prow;
+      const int lc = pch ^ (R & 7);  // logical chunk this lane fetches
+      const void* src = zero;
+      if (second) {
+        const int k = k0 + lc * 8;
+        if (m0 + R < g.M && k < g.K2) src = g.a2 + a2_off + (long)(m0 + R) * g.lda2 + k;
+      } else if (CONV) {
+        const ConvGeom& cv = g.conv;
+        if (rc[i].valid && ti.valid) {
+          int iy, ix;
+          bool ok;
+          if (CONV == PSO_CONV_NORMAL) {
+            iy = rc[i].oy * cv.stride + ti.kh - cv.pad;
+            ix = rc[i].ox * cv.stride + ti.kw - cv.pad;
+            ok = (unsigned)iy < (unsigned)cv.H && (unsigned)ix < (unsigned)cv.W;
+          } else if (CONV == PSO_CONV_UP2) {
+            const int uy = rc[i].oy + ti.kh - cv.pad, ux = rc[i].ox + ti.kw - cv.pad;
+            ok = (unsigned)uy < (unsigned)(2 * cv.H) && (unsigned)ux < (unsigned)(2 * cv.W);
+            iy = uy >> 1;
+            ix = ux >> 1;
+          } else {
+            const int ty = rc[i].oy + cv.pad - ti.kh, tx = rc[i].ox + cv.pad - ti.kw;
+            iy = ty >> 1;
+            ix = tx >> 1;
+            ok = ty >= 0 && tx >= 0 && !(ty & 1) && !(tx & 1) && iy < cv.H && ix < cv.W;
+          }
+          if (ok) src = ti.src + (((long)rc[i].b * cv.H + iy) * cv.W + ix) * ti.Cs + ti.c0 + lc * 8;
+        }
+      } else {
+        const int k = k0 + lc * 8;
+        if (m0 + R < g.M && k < g.K1) src = g.a1 + (long)(m0 + R) * g.lda1 + k;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < T::B_CH; ++i) {
-      const int q = tid + GEMM_THREADS * i;
-      const int row = q >> 3, kc = (q & 7) * 8;
-      rb[i] = second ? load_chunk_dense(g.b2, g.ldb2, n0 + row, g.N, k0 + kc, g.K2)
-                     : load_chunk_dense(g.b1, g.ldb1, n0 + row, g.N, k0 + kc, g.K1);
-    }
-  };
-  auto store_tile = [&](int buf) {
-    bf16_t* la = lds[buf];
-    bf16_t* lb = lds[buf] + BM * BK;
-#pragma unroll
-    for (int i = 0; i < T::A_CH; ++i) {
-      const int q = tid + GEMM_THREADS * i;
-      *reinterpret_cast<uint4*>(la + swz(q >> 3, q & 7)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < T::B_CH; ++i) {
-      const int q = tid + GEMM_THREADS * i;
-      *reinterpret_cast<uint4*>(lb + swz(q >> 3, q & 7)) = rb[i];
+      const int piece = wave * T::B_CH + i;
+      const int R = piece * 8 + prow;
+      const int lc = pch ^ (R & 7);
+      const int k = k0 + lc * 8;
+      const void* src = zero;
+      if (second) {
+        if (n0 + R < g.N && k < g.K2) src = g.b2 + (long)(n0 + R) * g.ldb2 + k;
+      } else {
+        if (n0 + R < g.N && k < g.K1) src = g.b1 + (long)(n0 + R) * g.ldb1 + k;
+      }
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(lb + piece * 8 * BK), 16, 0, 0);
     }
   };
 
@@ -205,44 +246,50 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
+  // prologue: K-tiles 0 .. STAGES-2 in flight; wait for tile 0
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nt) issue_tile(s, s);
+  if (STAGES == 3 && nt > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   const int fr = lane & 15, fk = lane >> 4;
+  int cur = 0;
   for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) load_tile(t + 1);
-    const bf16_t* la = lds[cur];
-    const bf16_t* lb = lds[cur] + BM * BK;
+    const bool ahead = t + STAGES - 1 < nt;
+    if (ahead) issue_tile(t + STAGES - 1, (cur + STAGES - 1) % STAGES);
+    const bf16_t* la = stage_ptr(cur);
+    const bf16_t* lb = stage_ptr(cur) + BM * BK;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[MI], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / 2) + i * 16 + fr, kk * 4 + fk));
+        af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / WM) + i * 16 + fr, kk * 4 + fk));
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / 2) + j * 16 + fr, kk * 4 + fk));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / WN) + j * 16 + fr, kk * 4 + fk));
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
-    if (t + 1 < nt) store_tile(cur ^ 1);
-    __syncthreads();
+    // K-tile t+1 must have landed (every wave's pieces) before anyone reads it; tiles beyond stay in flight
+    if (STAGES == 3 && ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    cur = (cur + 1 == STAGES) ? 0 : cur + 1;
   }
 
   // ---- epilogue: lane holds out[m][n0..n0+3] for each (i, j) ----
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * (BM / 2) + i * 16 + fr;
+    const int m = m0 + wm * (BM / WM) + i * 16 + fr;
     if (m >= g.M) continue;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 16 + fk * 4;
+      const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
       if (n >= g.N) continue;
       float v[4] = {acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
                     acc[i][j][3] * g.alpha};
@@ -294,15 +341,31 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs g) 
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2>
 static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   dim3 grid(nblk, ksplit);
+  const int threads = 64 * WM * WN;
+  const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
+  static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr_done = true;
+  }
   switch (g.conv.mode) {
-    case PSO_CONV_NORMAL: gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL><<<grid, GEMM_THREADS, 0, st>>>(g); break;
-    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2><<<grid, GEMM_THREADS, 0, st>>>(g); break;
-    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2><<<grid, GEMM_THREADS, 0, st>>>(g); break;
-    default: gemm_bf16_kernel<BM, BN, 0><<<grid, GEMM_THREADS, 0, st>>>(g);
+    case PSO_CONV_NORMAL:
+      gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES><<<grid, threads, shm, st>>>(g);
+      break;
+    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES><<<grid, threads, shm, st>>>(g); break;
+    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES><<<grid, threads, shm, st>>>(g); break;
+    default: gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES><<<grid, threads, shm, st>>>(g);
   }
   return pso_check_launch("pso_gemm");
 }
@@ -310,20 +373,49 @@ static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 
+static int g_gemm_variant = 0;  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
+
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
     pso_set_error("pso_gemm: tail_group_n must be a multiple of 64");
     return PSO_ERR_ARG;
   }
-  if (g.tail_group_n > 0 && (g.tail_group_n % 128) != 0) return launch<128, 64>(g, st);
   g.vec_ok = (g.ldo % 4) == 0 && (g.out_dtype == PSO_F32 ? al16(g.out) : al8(g.out)) &&
              (!g.resid || ((g.ldr % 4) == 0 && al8(g.resid))) && (!g.bias || al8(g.bias)) &&
              (!g.rowbias || (al8(g.rowbias) && (g.ld_rowbias % 4) == 0));
-  // Small-N / small-M shapes: 64-wide tiles waste less.
-  if (g.N <= 64) return launch<128, 64>(g, st);
+  const bool bn64_only = g.tail_group_n > 0 && (g.tail_group_n % 128) != 0;  // grouped tail needs BN | group
+  const bool bn256_ok = g.tail_group_n == 0 || (g.tail_group_n % 256) == 0;
+  const long Ktot = (long)g.K1 + (g.a2 ? g.K2 : 0);
+  // Small outputs with a long reduction: split K over blocks, f32 atomics in the epilogue.
+  const bool can_split = g.out_dtype == PSO_F32 && g.accumulate && !g.bias && !g.rowbias && !g.resid &&
+                         !g.conv.mode && g.tail_group_n == 0;
+  if (can_split && (g.M <= 128 || g.N <= 128) && Ktot >= 2048) {
+    const long tiles = (long)((g.M + 63) / 64) * ((g.N + 63) / 64);
+    const long ktiles = (Ktot + BK - 1) / BK;
+    long ks = (512 + tiles - 1) / tiles;
+    if (ks > ktiles / 2) ks = ktiles / 2;
+    if (ks < 1) ks = 1;
+    return launch<64, 64>(g, st, (int)ks);
+  }
+  if (g_gemm_variant == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
+  if (g_gemm_variant == 2 && !bn64_only) return launch<128, 128, 2, 2, 3>(g, st);
+  if (g_gemm_variant == 3 && !bn64_only) return launch<128, 128>(g, st);
+  // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
+  // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
+  // and the skinny LoRA projections N = r..3r).
+  auto tiles = [&](int bm, int bn) { return (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn); };
+  if (g.N <= 64) return launch<64, 64>(g, st);
+  if (bn64_only) return tiles(128, 64) >= 512 ? launch<128, 64>(g, st) : launch<64, 64>(g, st);
   if (g.M <= 64) return launch<64, 128>(g, st);
-  return launch<128, 128>(g, st);
+  // 256x256 block tile, 8 waves x (128x64): twice the MFMAs per LDS fragment read; wins once the grid covers most of
+  // the 256 CUs (one 128 KiB-LDS block per CU).
+  if (bn256_ok && tiles(256, 256) >= 180) return launch<256, 256, 2, 4, 2>(g, st);
+  if (tiles(128, 128) >= 1024) return launch<128, 128>(g, st);
+  if (tiles(64, 128) >= 512) return (g.N % 128 == 0) ? launch<64, 128>(g, st) : launch<128, 64>(g, st);
+  return launch<64, 64>(g, st);
 }
 
 // =====================================================================================================================
@@ -498,6 +590,8 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
   return run_gemm(g, (hipStream_t)stream);
 }
+
+void pso_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream) {

@@ -367,13 +367,21 @@ def split_channels(x, C1, add2=None):
     return y1, y2
 
 
-def nchw_to_nhwc(x):
-    """[B,C,H,W] fp32|bf16 -> [B,H,W,C] bf16."""
+def nchw_to_nhwc(x, pad_to=None, scale=1.0):
+    """[B,C,H,W] fp32|bf16 -> [B,H,W,Cp] bf16 (channels zero-padded to Cp, values times scale)."""
     B, C, H, W = x.shape
-    out = torch.empty((B, H, W, C), device=x.device, dtype=BF16)
-    check(lib().pso_nchw_to_nhwc(B, C, H * W, ptr(x.contiguous()), dtype_code(x), ptr(out), stream_ptr()),
-          "pso_nchw_to_nhwc")
+    Cp = pad_to or C
+    out = torch.empty((B, H, W, Cp), device=x.device, dtype=BF16)
+    check(lib().pso_nchw_to_nhwc(B, C, Cp, H * W, ptr(x.contiguous()), dtype_code(x), float(scale), ptr(out),
+                                 stream_ptr()), "pso_nchw_to_nhwc")
     return out
+
+
+def softmax_rows(x):
+    """in-place row softmax of a bf16 [M, N] matrix (row-strided view)."""
+    M, N = x.shape
+    check(lib().pso_softmax_rows(M, N, ptr(x), _row_stride(x), stream_ptr()), "pso_softmax_rows")
+    return x
 
 
 def nhwc_to_nchw(x, dtype=torch.float32):

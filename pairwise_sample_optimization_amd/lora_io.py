@@ -1,0 +1,84 @@
+"""LoRA checkpoint interchange in the diffusers format the reference writes and reads.
+
+* `save_lora_weights(output_dir, unet_lora_layers)` -- `StableDiffusionXLLoraLoaderMixin.save_lora_weights`
+  as used by the save hook `T:361-379`: `pytorch_lora_weights.safetensors`, keys `unet.<module>.lora.{down,up}.weight`
+  (peft `lora_A/lora_B` renamed by `convert_state_dict_to_diffusers`).
+* `lora_state_dict(input_dir)` / `load_lora_into_unet(sd, network_alphas, unet)` -- the load hook `T:381-395`
+  (and the consumers `T:138`, `evaluate_sdxl_dmd2.py:194`); accepts diffusers (`lora.down/up`) or peft
+  (`lora_A/lora_B`) naming, with or without the `unet.` prefix.
+* `save_state(trainer, dir)` / `load_state(trainer, dir)` -- resume (`T:886-890`, `accelerator.save_state`): the
+  LoRA file plus the AdamW moments and step count (`optimizer.safetensors`).
+"""
+import json
+import os
+
+import torch
+from safetensors.torch import load_file, save_file
+
+LORA_WEIGHT_NAME = "pytorch_lora_weights.safetensors"
+OPT_NAME = "optimizer.safetensors"
+
+
+def peft_to_diffusers(sd):
+    """convert_state_dict_to_diffusers for a peft LoRA state dict: `.lora_A.` -> `.lora.down.`, `.lora_B.` -> `.lora.up.`"""
+    out = {}
+    for k, v in sd.items():
+        out[k.replace(".lora_A.", ".lora.down.").replace(".lora_B.", ".lora.up.")] = v
+    return out
+
+
+def diffusers_to_peft(sd):
+    out = {}
+    for k, v in sd.items():
+        if k.startswith("unet."):
+            k = k[len("unet."):]
+        out[k.replace(".lora.down.", ".lora_A.").replace(".lora.up.", ".lora_B.")] = v
+    return out
+
+
+def get_peft_model_state_dict(unet):
+    return unet.lora.state_dict_peft()
+
+
+def save_lora_weights(output_dir, unet_lora_layers, weight_name=LORA_WEIGHT_NAME):
+    os.makedirs(output_dir, exist_ok=True)
+    packed = {f"unet.{k}": v.detach().float().contiguous().cpu() for k, v in unet_lora_layers.items()}
+    save_file(packed, os.path.join(output_dir, weight_name), metadata={"format": "pt"})
+
+
+def lora_state_dict(input_dir, weight_name=LORA_WEIGHT_NAME):
+    path = input_dir if input_dir.endswith(".safetensors") else os.path.join(input_dir, weight_name)
+    return load_file(path), None
+
+
+def load_lora_into_unet(state_dict, network_alphas, unet):
+    """Copy a LoRA state dict into the unet's adapter (ranks must match; network_alphas other than None/rank are
+    folded into B as alpha/r, like peft's scaling)."""
+    sd = diffusers_to_peft(state_dict)
+    st = unet.lora
+    missing = [n for n in st.adapter_names() if f"{n}.lora_A.weight" not in sd or f"{n}.lora_B.weight" not in sd]
+    if missing:
+        raise KeyError(f"LoRA state dict lacks {len(missing)} adapters, e.g. {missing[0]}")
+    dev = st.master.device
+    st.load_peft({k: v.to(dev, torch.float32) for k, v in sd.items()})
+
+
+def save_state(trainer, output_dir):
+    unet = trainer.unet
+    save_lora_weights(output_dir, peft_to_diffusers(get_peft_model_state_dict(unet)))
+    save_file({"exp_avg": trainer.exp_avg.cpu(), "exp_avg_sq": trainer.exp_avg_sq.cpu()},
+              os.path.join(output_dir, OPT_NAME),
+              metadata={"step": str(trainer.opt_step), "n_micro": str(trainer.n_micro)})
+    with open(os.path.join(output_dir, "pso_state.json"), "w") as f:
+        json.dump({"opt_step": trainer.opt_step, "n_micro": trainer.n_micro, "rank": unet.lora.r}, f)
+
+
+def load_state(trainer, input_dir):
+    sd, alphas = lora_state_dict(input_dir)
+    load_lora_into_unet(sd, alphas, trainer.unet)
+    opt = load_file(os.path.join(input_dir, OPT_NAME))
+    trainer.exp_avg.copy_(opt["exp_avg"])
+    trainer.exp_avg_sq.copy_(opt["exp_avg_sq"])
+    with open(os.path.join(input_dir, "pso_state.json")) as f:
+        meta = json.load(f)
+    trainer.opt_step, trainer.n_micro = int(meta["opt_step"]), int(meta["n_micro"])

