@@ -118,6 +118,15 @@ def cpu_baseline(args, unet):
                       f"{dt:.1f} s"}
 
 
+def max_over_ranks(dt, dev):
+    """The slowest rank sets the job time (barrier-bracketed timed region, MAX over ranks)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return dt
+    tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return tt.item()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,10 +155,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
+    dt = max_over_ranks(dt, dev)
     imgs_per_step_gpu = 2 * args.pairs * args.gas * (args.num_steps - 1)
     value = imgs_per_step_gpu * world * args.steps / dt
     ms = dt / args.steps * 1e3

@@ -34,6 +34,42 @@ def compute_time_ids(size, crop=0, device=None):
     return torch.tensor([[size, size, crop, crop, size, size]], dtype=torch.float32, device=device)
 
 
+def shuffle_index(perm, perms, P):
+    """Row indices of the shuffled, re-batched training stream (T:733-760 / D:719-753).
+
+    perm [Bp] pair permutation, perms [Bp, T] per-row time permutation.  The reference applies `perms` after
+    `samples = samples[perm]`, so shuffled row i = old pair perm[i] with time order perms[i].  Micro-step s = (batch b, step j) holds, for p < P and
+    member k, buffer row ((perm[bP+p]*2 + k)*T + perms[bP+p, j]) of the [2Bp*T] latent stream.
+    Returns (img_idx [nb*T*P*2], pair_img [same] rows of per-pair tensors, tsel [same] transition index)."""
+    Bp, T = perms.shape
+    nb = Bp // P
+    dev = perm.device
+    pb = torch.arange(nb, device=dev).view(nb, 1, 1, 1)
+    jj = torch.arange(T, device=dev).view(1, T, 1, 1)
+    pp = torch.arange(P, device=dev).view(1, 1, P, 1)
+    kk = torch.arange(2, device=dev).view(1, 1, 1, 2)
+    row = pb * P + pp                                         # new (shuffled) position  [nb,1,P,1]
+    pair = perm[row]                                          # old pair id
+    tsel = perms[row, jj]                                     # [nb,T,P,1]
+    img_idx = ((pair * 2 + kk) * T + tsel).reshape(-1)
+    pair_img = (pair * 2 + kk).expand(nb, T, P, 2).reshape(-1)
+    tsel_i = tsel.expand(nb, T, P, 2).reshape(-1)
+    return img_idx, pair_img, tsel_i
+
+
+def allreduce_grads(flat, process_group=None):
+    """DDP gradient sync of the flat LoRA grad bucket (T:857 under accelerate: all-reduce SUM, then the mean).  The
+    1/world factor is returned, not applied: the clip and AdamW kernels fold it into their gradient read, so the
+    bucket is touched once by RCCL and once by the optimizer."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    world = dist.get_world_size(process_group)
+    if world == 1:
+        return 1.0
+    dist.all_reduce(flat, group=process_group)
+    return 1.0 / world
+
+
 class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
@@ -175,15 +211,7 @@ class PSOTrainer:
         perm = torch.randperm(Bp, device=dev, generator=generator)
         perms = torch.argsort(torch.rand((Bp, T), device=dev, generator=generator), dim=1)  # per-pair time perm
         nb = Bp // P
-        pb = torch.arange(nb, device=dev).view(nb, 1, 1, 1)
-        jj = torch.arange(T, device=dev).view(1, T, 1, 1)
-        pp = torch.arange(P, device=dev).view(1, 1, P, 1)
-        kk = torch.arange(2, device=dev).view(1, 1, 1, 2)
-        pair = perm[pb * P + pp]                                  # [nb,1,P,1]
-        tsel = perms[pair, jj]                                    # [nb,T,P,1]
-        img_idx = ((pair * 2 + kk) * T + tsel).reshape(-1)        # rows of [2Bp*T]
-        pair_img = (pair * 2 + kk).expand(nb, T, P, 2).reshape(-1)  # rows of [2Bp]
-        tsel_i = tsel.expand(nb, T, P, 2).reshape(-1)
+        img_idx, pair_img, tsel_i = shuffle_index(perm, perms, P)
         tt = self.timesteps_dev[tsel_i]
         out = SimpleNamespace(n_micro=nb * T, P=P)
         flat = lambda t: t.reshape((n_img * T,) + tuple(t.shape[2:]))
@@ -242,10 +270,7 @@ class PSOTrainer:
     # ------------------------------------------------------------------------------------------------------------
     def optimizer_step(self):
         st = self.unet.lora
-        scale = 1.0
-        if self.world > 1:
-            dist.all_reduce(st.grad, group=self.pg)  # one flat bucket over xGMI; mean folded into grad_scale
-            scale = 1.0 / self.world
+        scale = allreduce_grads(st.grad, self.pg)
         K.grad_clip_coef(st.grad, self.max_grad_norm, grad_scale=scale, out=self.clip_buf)
         self.opt_step += 1
         K.adamw_step(st.master, st.grad, self.exp_avg, self.exp_avg_sq, self.lr, self.betas, self.adam_eps, self.wd,

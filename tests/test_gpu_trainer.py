@@ -112,3 +112,36 @@ def test_optimizer_step_matches_torch_adamw(cuda):
         clip = K.grad_clip_coef(gg, 1.0)
         K.adamw_step(p, gg, m, v, 1e-3, (0.9, 0.999), 1e-8, 1e-2, step, clip=clip)
     assert (p - p_ref.detach()).abs().max().item() < 1e-5
+
+
+def test_checkpoint_save_load_roundtrip(cuda, tmp_path):
+    """save_state -> fresh trainer -> load_state restores LoRA weights, AdamW moments and counters (T:886-890)."""
+    from pairwise_sample_optimization_amd import lora_io
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    mk = lambda: UNet2DConditionModel(UNetConfig.tiny(16))
+    with torch.device(cuda):
+        u1, u2 = mk(), mk()
+    u1.init_weights(0)
+    u2.init_weights(0)
+    u1.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+    u2.add_adapter(SimpleNamespace(r=8, lora_alpha=8, seed=5))
+    u1.lora.init_gaussian(1, b_std=1e-2)
+    t1 = PSOTrainer(u1, mode="turbo", num_steps=4)
+    t2 = PSOTrainer(u2, mode="turbo", num_steps=4)
+    t1.exp_avg.normal_()
+    t1.exp_avg_sq.uniform_()
+    t1.opt_step, t1.n_micro = 7, 21
+    lora_io.save_state(t1, str(tmp_path))
+    lora_io.load_state(t2, str(tmp_path))
+    assert torch.equal(u1.lora.master, u2.lora.master)
+    assert torch.equal(t1.exp_avg, t2.exp_avg) and torch.equal(t1.exp_avg_sq, t2.exp_avg_sq)
+    assert (t2.opt_step, t2.n_micro) == (7, 21)
+    x = torch.randn(2, 4, 16, 16, device=cuda)
+    enc = torch.randn(2, 77, 128, device=cuda)
+    cond = {"text_embeds": torch.randn(2, 64, device=cuda),
+            "time_ids": torch.tensor([[128.0, 128, 0, 0, 128, 128]] * 2, device=cuda)}
+    with torch.no_grad():
+        e1 = u1(x, 999.0, enc, added_cond_kwargs=cond).sample
+        e2 = u2(x, 999.0, enc, added_cond_kwargs=cond).sample
+    assert torch.equal(e1, e2)

@@ -1,0 +1,61 @@
+"""CPU checks of the host-side mirrors of the reference surface: run configs, LoRA key layout / checkpoint format,
+trainer construction rules.  No GPU compute."""
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+
+def test_configs_match_reference_values():
+    from pairwise_sample_optimization_amd.config import config_sdxl_dmd_dpo, config_sdxl_turbo_dpo
+    t = config_sdxl_turbo_dpo.get_config()
+    d = config_sdxl_dmd_dpo.get_config()
+    # config_sdxl_turbo_dpo.py:64-119 / config_sdxl_dmd_dpo.py
+    assert (t.sample.num_steps, t.train.distilled_train_steps, t.train.beta, t.train.eps) == (4, 3, 50, 0.1)
+    assert (t.train.lora_rank, t.train.batch_size, t.train.gradient_accumulation_steps) == (32, 4, 2)
+    assert (d.train.lora_rank, d.train.batch_size, d.train.gradient_accumulation_steps) == (16, 1, 4)
+    assert t.pretrained.pretrained_model_name_or_path == "stabilityai/sdxl-turbo"
+    assert d.reward_fn == "pickscore+imagereward" and t.reward_fn == "pick_score"
+    with pytest.raises(AttributeError):
+        t.train.no_such_key
+    t.train.learning_rate = 3e-5
+    assert t.to_dict()["train"]["learning_rate"] == 3e-5
+
+
+def test_trainer_from_config_enforces_T():
+    from pairwise_sample_optimization_amd.config import config_sdxl_turbo_dpo
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer
+    c = config_sdxl_turbo_dpo.get_config()
+    c.train.distilled_train_steps = 2  # T:221 assert: must be num_steps - 1
+    with pytest.raises(AssertionError):
+        PSOTrainer.from_config(None, c)
+
+
+def test_sdxl_lora_adapter_layout_and_diffusers_keys():
+    from pairwise_sample_optimization_amd import lora_io
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    with torch.device("meta"):
+        u = UNet2DConditionModel(UNetConfig.sdxl())
+    st = u.add_adapter(SimpleNamespace(r=32, lora_alpha=32))
+    names = list(st.adapter_names())
+    assert len(names) == 70 * 2 * 4          # 70 transformer blocks x (attn1, attn2) x (q, k, v, out.0)
+    assert st.master.numel() == 46_448_640   # 46.45 M LoRA params at r=32
+    sd = st.state_dict_peft()
+    diff = lora_io.peft_to_diffusers(sd)
+    k = "mid_block.attentions.0.transformer_blocks.9.attn2.to_out.0.lora.up.weight"
+    assert k in diff and diff[k].shape == (1280, 32)
+    assert diff["down_blocks.1.attentions.0.transformer_blocks.0.attn2.to_k.lora.down.weight"].shape == (32, 2048)
+    back = lora_io.diffusers_to_peft({f"unet.{kk}": v for kk, v in diff.items()})
+    assert set(back) == set(sd)
+
+
+def test_lora_safetensors_format(tmp_path):
+    from safetensors.torch import load_file
+    from pairwise_sample_optimization_amd import lora_io
+    sd = {"a.attn1.to_q.lora_A.weight": torch.randn(4, 8), "a.attn1.to_q.lora_B.weight": torch.randn(8, 4)}
+    lora_io.save_lora_weights(str(tmp_path), lora_io.peft_to_diffusers(sd))
+    raw = load_file(str(tmp_path / lora_io.LORA_WEIGHT_NAME))
+    assert set(raw) == {"unet.a.attn1.to_q.lora.down.weight", "unet.a.attn1.to_q.lora.up.weight"}
+    got, alphas = lora_io.lora_state_dict(str(tmp_path))
+    assert alphas is None
+    assert torch.equal(lora_io.diffusers_to_peft(got)["a.attn1.to_q.lora_B.weight"], sd["a.attn1.to_q.lora_B.weight"])
