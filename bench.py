@@ -11,6 +11,7 @@ rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling), RCC
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (torchrun sets RANK/WORLD_SIZE/LOCAL_RANK)
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -83,14 +84,25 @@ def roofline(tr, buf, g):
     one_step(tr, buf, g)
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
-    fl = sum(f for f, _, _ in rec)
-    ms = sum(a.elapsed_time(b) for _, a, b in rec)
+    fl = sum(r[0] for r in rec)
+    nb = sum(r[1] for r in rec)
+    ms = sum(r[2].elapsed_time(r[3]) for r in rec)
     n = len(rec)
     achieved = fl / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": "gemm_bf16_kernel (all GEMM + implicit-GEMM conv launches)",
-            "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "launches_per_step": n,
-            "flop_per_step": fl, "avg_launch_us": round(ms * 1e3 / max(n, 1), 2)}
+    out = {"bound": "mfma", "kernel": "gemm_bf16_kernel<...> + gemm_tn_kernel (every GEMM / implicit-GEMM conv "
+                                      "launch of one train step)",
+           "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "launches_per_step": n,
+           "flop_per_launch": fl / max(n, 1), "bytes_per_launch": nb / max(n, 1),
+           "avg_launch_us": round(ms * 1e3 / max(n, 1), 2)}
+    # HBM bytes per launch from the PMC passes of the same command (tools/gpu_full.sh -> tools/parse_prof.py)
+    tp = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
+    if tp:
+        t = json.load(open(tp[-1]))
+        out["traffic"] = round(t["traffic_bytes_per_launch"])
+        out["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)"
+        out["traffic_source"] = os.path.relpath(tp[-1], os.path.dirname(os.path.abspath(__file__)))
+    return out
 
 
 def cpu_baseline(args, unet):

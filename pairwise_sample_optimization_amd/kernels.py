@@ -24,11 +24,12 @@ def _prof_begin():
     return e0
 
 
-def _prof_end(e0, flops):
+def _prof_end(e0, flops, nbytes=0.0, tag=None):
+    """nbytes: algorithmic HBM bytes of the launch (every operand read once, the output written once)."""
     if e0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        PROFILE.append((flops, e0, e1))
+        PROFILE.append((flops, nbytes, e0, e1, tag))
 
 
 def _row_stride(t):
@@ -59,7 +60,9 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
                          int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
                          ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
                          stream_ptr()), "pso_gemm")
-    _prof_end(e0, 2.0 * M * N * (K1 + K2))
+    _prof_end(e0, 2.0 * M * N * (K1 + K2),
+              2.0 * (M * (K1 + (a2.shape[1] if a2 is not None else 0)) + N * (K1 + K2)) + out.element_size() * M * N,
+              ("gemm", M, N, K1, K2, tail_group_n, out.dtype == torch.float32))
     return out
 
 
@@ -71,7 +74,7 @@ def gemm_tn(a, b, out, alpha=1.0):
     e0 = _prof_begin()
     check(lib().pso_gemm_tn(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
                             _row_stride(out), stream_ptr()), "pso_gemm_tn")
-    _prof_end(e0, 2.0 * M * I * J)
+    _prof_end(e0, 2.0 * M * I * J, 2.0 * M * (I + J) + 8.0 * I * J, ("gemm_tn", M, I, J))
     return out
 
 
@@ -106,7 +109,9 @@ def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=N
                            ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
                            ptr(resid), Cout if resid is not None else 0, ptr(out), ldo, dtype_code(out),
                            int(accumulate), stream_ptr()), "pso_conv2d")
-    _prof_end(e0, 2.0 * B * Ho * Wo * Cout * (ks * ks * (C1 + C2) + K2))
+    _prof_end(e0, 2.0 * B * Ho * Wo * Cout * (ks * ks * (C1 + C2) + K2),
+              2.0 * (B * H * W * (C1 + C2) + Cout * ks * ks * (C1 + C2) + B * Ho * Wo * K2 + Cout * K2)
+              + out.element_size() * B * Ho * Wo * Cout, ("conv", mode, B, H, W, C1, C2, Cout, ks, stride, K2))
     return out
 
 

@@ -1,0 +1,39 @@
+"""Per-shape breakdown of the GEMM family inside one C2 train step (HIP events per launch, grouped by shape).
+usage: python tools/shape_prof.py [--top 40]  (GPU)"""
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from pairwise_sample_optimization_amd import kernels as K  # noqa: E402
+
+
+def main():
+    sys.argv = [sys.argv[0], "--no-cpu-baseline"] + sys.argv[1:]
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    unet, tr, buf, g = bench.build(args, dev)
+    bench.one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    K.PROFILE = []
+    bench.one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    rec, K.PROFILE = K.PROFILE, None
+    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    for fl, nb, e0, e1, tag in rec:
+        a = agg[tag]
+        a[0] += 1
+        a[1] += e0.elapsed_time(e1)
+        a[2] += fl
+    tot = sum(a[1] for a in agg.values())
+    print(f"GEMM family: {len(rec)} launches, {tot:.1f} ms, {sum(a[2] for a in agg.values()) / tot / 1e9:.1f} TF/s")
+    for tag, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
+        print(f"{ms:8.2f} ms {100 * ms / tot:5.1f}% n={n:4d} {fl / ms / 1e9:7.1f} TF/s  {tag}")
+
+
+if __name__ == "__main__":
+    main()
