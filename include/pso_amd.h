@@ -102,6 +102,8 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
 /* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
  * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage). */
 void pso_gemm_set_variant(int v);
+/* Benchmark knob: split count of pso_gemm_tn over the reduction rows (0 = automatic). */
+void pso_gemm_tn_set_split(int ks);
 
 /* TN GEMM, f32 accumulate: out[I][J] += alpha * sum_m A[m][I] * B[m][J] (A [M][I], B [M][J] row-major, row strides
  * lda/ldb; I, J multiples of 8).  Replaces the peft LoRA weight-gradient GEMMs of the backward (dA = v^T x,

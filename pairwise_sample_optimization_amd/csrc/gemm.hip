@@ -349,13 +349,13 @@ static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
   static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
@@ -373,7 +373,11 @@ static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 
-static int g_gemm_variant = 0;  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
+int pso_gemm_skinny_nt(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha, void* out,
+                       long ldo, int out_f32, int accumulate, hipStream_t st);
+
+static int g_gemm_variant = 0;
+static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
@@ -387,6 +391,11 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const bool bn64_only = g.tail_group_n > 0 && (g.tail_group_n % 128) != 0;  // grouped tail needs BN | group
   const bool bn256_ok = g.tail_group_n == 0 || (g.tail_group_n % 256) == 0;
   const long Ktot = (long)g.K1 + (g.a2 ? g.K2 : 0);
+  // Skinny N (the LoRA rank-r products): one 16-row x all-N tile per 4-wave block, K split over the waves.
+  if (g_gemm_variant == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
+      (g.N % 4) == 0 && g.vec_ok && g.M >= 256)
+    return pso_gemm_skinny_nt(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.alpha, g.out, g.ldo,
+                              g.out_dtype == PSO_F32, g.accumulate, st);
   // Small outputs with a long reduction: split K over blocks, f32 atomics in the epilogue.
   const bool can_split = g.out_dtype == PSO_F32 && g.accumulate && !g.bias && !g.rowbias && !g.resid &&
                          !g.conv.mode && g.tail_group_n == 0;
@@ -592,6 +601,7 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
 }
 
 void pso_gemm_set_variant(int v) { g_gemm_variant = v; }
+void pso_gemm_tn_set_split(int ks) { g_tn_split = ks; }
 
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream) {
@@ -601,7 +611,9 @@ int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, lon
   if (M == 0) return PSO_OK;
   const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
   const int nkt = (M + 63) / 64;
-  int ks = (512 + tiles - 1) / tiles;
+  // ~160 blocks: fewer leaves the M-range latency-bound, more multiplies the f32 atomics (measured optimum on the
+  // LoRA dW shapes, M = 4096 / 16384, I x J = 1280x32 .. 640x32)
+  int ks = g_tn_split > 0 ? g_tn_split : (160 + tiles - 1) / tiles;
   if (ks > nkt) ks = nkt;
   if (ks < 1) ks = 1;
   gemm_tn_kernel<<<dim3(tiles, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B,

@@ -73,7 +73,7 @@ def allreduce_grads(flat, process_group=None):
 class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
-                 train_batch_size=1, num_reward=1, process_group=None):
+                 train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16):
         self.unet = unet
         self.mode = MODE_TURBO if mode == "turbo" else MODE_DMD
         self.num_steps = num_steps
@@ -94,6 +94,7 @@ class PSOTrainer:
         self.n_micro = 0
         self.clip_buf = torch.zeros(2, device=st.master.device, dtype=torch.float32)
         self.loss_hist = []
+        self.max_pass_images = max_pass_images  # images per batched UNet pass (HBM budget: ~5 GB saved each @1024^2)
         self.auto_step = True  # run the optimizer every gas*T micro-steps (tests may inspect raw grads)
         if self.mode == MODE_TURBO:
             self.sched = EulerAncestralDiscreteScheduler()
@@ -230,17 +231,27 @@ class PSOTrainer:
         out.rewards = out.rewards.contiguous()
         return out
 
-    def micro_batch(self, sb, s):
+    def micro_batch(self, sb, s, count=1):
+        """Micro-steps [s, s + count) of the shuffled stream (contiguous rows: 2P images per micro-step)."""
         n = 2 * self.P
-        sl = slice(s * n, (s + 1) * n)
+        sl = slice(s * n, (s + count) * n)
         return SimpleNamespace(x=sb.x[sl], x_next=sb.x_next[sl], unet_in=sb.unet_in[sl], enc=sb.enc[sl],
                                pooled=sb.pooled[sl], tid=sb.tid[sl], t=sb.t[sl], coef=sb.coef[sl],
-                               rewards=sb.rewards[s * self.P:(s + 1) * self.P])
+                               rewards=sb.rewards[s * self.P:(s + count) * self.P], count=count)
 
     # ------------------------------------------------------------------------------------------------------------
     # MICRO-STEP (T:773-861) -- no host synchronisation
     # ------------------------------------------------------------------------------------------------------------
     def micro_step(self, mb, generator=None):
+        """One micro-step, or -- when mb holds `count` consecutive micro-steps of ONE accumulation window -- all of
+        them in a single batched pass.  Inside a window the LoRA weights do not change (the optimizer steps only at
+        the window end, T:857-861), so the batched pass produces the sum of the per-micro-step gradients: every
+        pair's loss term keeps its weight 1 / (P * gas * T) (the per-micro-step mean over P pairs, divided by the
+        accumulation count as accelerate does).  Larger batches keep the MFMA GEMMs fed (M = images * tokens)."""
+        count = getattr(mb, "count", 1)
+        if self.n_micro // self.gas_total != (self.n_micro + count - 1) // self.gas_total:
+            raise ValueError("a batched pass must not cross an optimizer step")
+        P = self.P * count
         u = self.unet
         u.enable_adapters()
         eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
@@ -250,17 +261,17 @@ class PSOTrainer:
         u.enable_adapters()
         idx = None
         if self.mode == MODE_TURBO and self.m > 1:  # sample_compare draws a reward column per pair (T:405)
-            idx = torch.randint(0, self.m, (self.P,), device=mb.x.device, generator=generator)
+            idx = torch.randint(0, self.m, (P,), device=mb.x.device, generator=generator)
         pref = K.preference(mb.rewards, 0 if self.mode == MODE_TURBO else 1, reward_idx=idx)
-        ws = K.pair_loss_ws(self.P, mb.x[0].numel(), mb.x.device)
+        ws = K.pair_loss_ws(P, mb.x[0].numel(), mb.x.device)
         loss, lp = K.pair_loss_fwd(self.mode, mb.x, mb.x_next, eps_pol, eps_ref, mb.coef, pref, self.beta,
                                    self.clip_eps, ws)
         # accelerator.backward divides by gradient_accumulation_steps (accelerate accelerator.py:2840)
         deps = K.pair_loss_bwd(self.mode, mb.x, mb.x_next, eps_pol, mb.coef, pref, self.beta, self.clip_eps, ws,
-                               grad_scale=1.0 / self.gas_total)
+                               grad_scale=count / self.gas_total)
         u.backward_nhwc(deps, rt)
-        self.loss_hist.append(loss)
-        self.n_micro += 1
+        self.loss_hist.append(loss)  # mean over the pass's pairs = mean of its micro-step losses
+        self.n_micro += count
         if self.auto_step and self.n_micro % self.gas_total == 0:
             self.optimizer_step()
         return loss
@@ -278,7 +289,13 @@ class PSOTrainer:
         K.zero_(st.grad)
         st.refresh()
 
-    def train_epoch(self, sb):
-        """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861)."""
-        for s in range(sb.n_micro):
-            self.micro_step(self.micro_batch(sb, s))
+    def train_epoch(self, sb, generator=None):
+        """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861), batched per accumulation
+        window up to `max_pass_images` images per UNet pass."""
+        s = 0
+        per_pass = max(1, self.max_pass_images // (2 * self.P))
+        while s < sb.n_micro:
+            left_in_window = self.gas_total - self.n_micro % self.gas_total
+            c = min(per_pass, left_in_window, sb.n_micro - s)
+            self.micro_step(self.micro_batch(sb, s, c), generator=generator)
+            s += c

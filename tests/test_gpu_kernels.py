@@ -174,3 +174,22 @@ def test_conv_every_variant_large(cuda, variant):
         assert _rel(_nchw(out), ref) < 1e-5
     finally:
         K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 32, 1280), (4096, 96, 1280), (16384, 32, 640), (300, 100, 136),
+                                   (1000, 64, 2048), (257, 128, 72), (4096, 4, 40)])
+def test_gemm_skinny_n(cuda, M, N, K):
+    """LoRA-rank products (N <= 128): bf16 out, strided A view, f32 accumulate; ragged M / K tails."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    big = torch.randn(M, K + 24, device=cuda, generator=g).bfloat16()
+    a = big[:, 16:16 + K]
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    ref = a.float() @ w.float().t()
+    out = K_.gemm(a, w, alpha=0.5)
+    assert out.shape == (M, N)
+    assert _rel(out, 0.5 * ref) < 4e-3
+    acc = torch.randn(M, N, device=cuda, generator=g)
+    want = acc + ref
+    K_.gemm(a, w, out=acc, out_dtype=torch.float32, accumulate=True)
+    assert _rel(acc, want) < 1e-5

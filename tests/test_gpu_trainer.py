@@ -145,3 +145,58 @@ def test_checkpoint_save_load_roundtrip(cuda, tmp_path):
         e1 = u1(x, 999.0, enc, added_cond_kwargs=cond).sample
         e2 = u2(x, 999.0, enc, added_cond_kwargs=cond).sample
     assert torch.equal(e1, e2)
+
+
+@pytest.mark.parametrize("mode", ["turbo", "dmd"])
+def test_batched_window_equals_sequential_micro_steps(cuda, mode):
+    """One batched pass over a whole accumulation window == the reference's sequential micro-steps
+    (T:755-861): same summed LoRA gradient (up to fp32 summation order and bf16 tile effects), same mean loss."""
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+    unet.lora.init_gaussian(seed=1, b_std=0.05)
+    P, gas, N = 2, 2, 3
+    tr = PSOTrainer(unet, mode=mode, num_steps=N, gradient_accumulation_steps=gas, train_batch_size=P,
+                    num_reward=2)
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Bp = P * gas
+    enc = torch.randn(Bp, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(Bp, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(128, 0, cuda).repeat(Bp, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, 16, generator=g,
+                          reward_fn=lambda x: torch.rand(x.shape[0], 2, device=cuda, generator=g))
+    sb = tr.shuffle(buf, generator=g)
+    assert sb.n_micro == gas * (N - 1) == tr.gas_total
+    st = unet.lora
+    st.grad.zero_()
+    g1 = torch.Generator(device="cuda").manual_seed(9)
+    seq = [tr.micro_step(tr.micro_batch(sb, s), generator=g1) for s in range(sb.n_micro)]
+    seq_grad = st.grad.clone()
+    seq_loss = torch.stack(seq).mean().item()
+    st.grad.zero_()
+    tr.n_micro = 0
+    g1 = torch.Generator(device="cuda").manual_seed(9)
+    # the reward column draws (turbo, T:405) come from one generator call instead of gas*T: draw them the same way
+    if mode == "turbo":
+        idx = torch.cat([torch.randint(0, 2, (P,), device=cuda, generator=g1) for _ in range(sb.n_micro)])
+        g1 = None
+        saved = torch.randint
+        torch.randint = lambda *a, **k: idx
+    try:
+        loss = tr.micro_step(tr.micro_batch(sb, 0, sb.n_micro), generator=g1)
+    finally:
+        if mode == "turbo":
+            torch.randint = saved
+    rel = ((st.grad - seq_grad).norm() / seq_grad.norm()).item()
+    print(f"{mode}: batched-vs-sequential grad rel {rel:.2e}, loss {loss.item():.6f} vs {seq_loss:.6f}")
+    assert seq_grad.norm() > 0
+    assert rel < 2e-2
+    assert abs(loss.item() - seq_loss) < 2e-3 * abs(seq_loss) + 1e-6
+    with pytest.raises(ValueError):
+        tr.n_micro = 1
+        tr.micro_step(tr.micro_batch(sb, 0, sb.n_micro))

@@ -22,7 +22,7 @@ def t_ms(fn, it=20):
 
 def main():
     dev = torch.device("cuda")
-    for v in (0,):
+    for v in [int(x) for x in os.environ.get("GEMM_VARIANTS", "0").split(",")]:
         K.lib().pso_gemm_set_variant(v)
         print(f"--- variant {v} ---")
         run(dev)
@@ -30,9 +30,9 @@ def main():
 
 def run(dev):
     rows = []
-    for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (16384, 5120 * 2, 640, "L1 ff.proj"),
+    for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (16384, 5120, 640, "L1 ff.proj"),
                              (16384, 640, 2560, "L1 ff.out"), (16384, 1920, 640, "L1 qkv"),
-                             (16384, 640, 640, "L1 out/proj"), (4096, 10240 * 2, 1280, "L2 ff.proj"),
+                             (16384, 640, 640, "L1 out/proj"), (4096, 10240, 1280, "L2 ff.proj"),
                              (4096, 1280, 5120, "L2 ff.out"), (4096, 3840, 1280, "L2 qkv"),
                              (4096, 1280, 1280, "L2 proj"), (4096, 96, 1280, "L2 lora u qkv"),
                              (4096, 32, 1280, "L2 lora v"), (16384, 32, 640, "L1 lora v")]:
