@@ -100,7 +100,8 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
              int tail_group_n, void* stream);
 
 /* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
- * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage). */
+ * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
+ * 6 = 64x128 (4 waves), 7 = 128x256 (8 waves), 8 = 128x128 (8 waves). */
 void pso_gemm_set_variant(int v);
 /* Benchmark knob: split count of pso_gemm_tn over the reduction rows (0 = automatic). */
 void pso_gemm_tn_set_split(int ks);

@@ -117,12 +117,20 @@ __device__ __attribute__((aligned(16))) uint4 g_zero16[4];  // source of every z
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// s_waitcnt the compiler's waitcnt pass can see (inline asm is opaque to it).  The builtin exists only in the device
+// compilation; the host pass must not see it or the kernel stubs are silently dropped.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PSO_S_WAITCNT(imm) __builtin_amdgcn_s_waitcnt(imm)
+#else
+#define PSO_S_WAITCNT(imm) ((void)0)
+#endif
+
 // Direct-to-LDS staging (global_load_lds_dwordx4): wave w fills 8-row x 128-B pieces; lane i of a piece lands at
 // byte 16*i of it (row i/8, physical chunk i%8), so the XOR swizzle is applied to the SOURCE chunk: physical chunk p of
 // row R holds logical chunk p ^ (R & 7) -- the same involution swz() applies on the read side.
 // WM x WN waves, each owning a (BM/WM) x (BN/WN) accumulator tile; STAGES-deep LDS ring with STAGES-1 K-tiles of
 // direct-to-LDS loads in flight behind a counted vmcnt and a raw s_barrier (a __syncthreads() would drain them).
-template <int BM, int BN, int CONV, int WM, int WN, int STAGES>
+template <int BM, int BN, int CONV, int WM, int WN, int STAGES, bool PIPE = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int WAVES = WM * WN;
   using T = Tile<BM, BN, WAVES>;
@@ -159,84 +167,109 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   const int nt = t_end > t_beg ? t_end - t_beg : 0;
   const long a2_off = g.tail_group_n > 0 ? (long)(n0 / g.tail_group_n) * g.K2 : 0;
 
-  // this lane's staging rows: piece j of wave w covers rows (w*PIECES + j)*8 .. +8
+  // This lane's staging rows: piece i of wave w covers rows (w*A_CH + i)*8 .. +8 (B likewise).  Rows past M / N are
+  // clamped onto the last valid row (their results are never stored), so the hot loop needs no row predicates and
+  // every per-tile address is (per-lane constant offset) + k0: no branches, no kernel-argument reloads.
   const int prow = lane >> 3;
   const int pch = lane & 7;
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero16);
+  const bf16_t* const a1 = g.a1;
+  const bf16_t* const b1 = g.b1;
+  const int K1 = g.K1;
+  int lcA[T::A_CH], offA[T::A_CH];  // logical chunk (source-side swizzle) and element offset of this lane's rows
+  int lcB[T::B_CH], offB[T::B_CH];
   RowCoord rc[T::A_CH];
-  if (CONV) {
 #pragma unroll
-    for (int i = 0; i < T::A_CH; ++i) {
-      const int R = (wave * T::A_CH + i) * 8 + prow;
-      const int m = m0 + R;
+  for (int i = 0; i < T::A_CH; ++i) {
+    const int R = (wave * T::A_CH + i) * 8 + prow;
+    const int m = min(m0 + R, g.M - 1);
+    lcA[i] = pch ^ (R & 7);
+    offA[i] = CONV ? 0 : (int)((long)m * g.lda1) + lcA[i] * 8;
+    if (CONV) {
       const int hw = g.conv.Ho * g.conv.Wo;
-      rc[i].valid = m < g.M;
-      const int mm = rc[i].valid ? m : 0;
-      rc[i].b = mm / hw;
-      const int rem = mm - rc[i].b * hw;
+      rc[i].valid = true;
+      rc[i].b = m / hw;
+      const int rem = m - rc[i].b * hw;
       rc[i].oy = rem / g.conv.Wo;
       rc[i].ox = rem - rc[i].oy * g.conv.Wo;
     }
   }
-  const uint4* zero = g_zero16;
+#pragma unroll
+  for (int i = 0; i < T::B_CH; ++i) {
+    const int R = (wave * T::B_CH + i) * 8 + prow;
+    const int n = min(n0 + R, g.N - 1);
+    lcB[i] = pch ^ (R & 7);
+    offB[i] = (int)((long)n * g.ldb1) + lcB[i] * 8;
+  }
+  // conv geometry in registers once
+  const int cvH = g.conv.H, cvW = g.conv.W, cvS = g.conv.stride, cvP = g.conv.pad;
 
   auto issue_tile = [&](int tt, int buf) {
     const int t = tt + t_beg;
-    const bool second = t >= nt1;
-    const int k0 = (second ? t - nt1 : t) * BK;
-    TapInfo ti;
-    if (CONV && !second) ti = tap_info(g, k0);
     bf16_t* la = stage_ptr(buf);
     bf16_t* lb = stage_ptr(buf) + BM * BK;
+    if (t < nt1) {
+      const int k0 = t * BK;
+      const bool full = k0 + BK <= K1;  // uniform: partial last K-tile needs per-chunk predicates
+      if (CONV) {
+        const TapInfo ti = tap_info(g, k0);
 #pragma unroll
-    for (int i = 0; i < T::A_CH; ++i) {
-      const int piece = wave * T::A_CH + i;
-      const int R = piece * 8 + prow;
-      const int lc = pch ^ (R & 7);  // logical chunk this lane fetches
-      const void* src = zero;
-      if (second) {
-        const int k = k0 + lc * 8;
-        if (m0 + R < g.M && k < g.K2) src = g.a2 + a2_off + (long)(m0 + R) * g.lda2 + k;
-      } else if (CONV) {
-        const ConvGeom& cv = g.conv;
-        if (rc[i].valid && ti.valid) {
+        for (int i = 0; i < T::A_CH; ++i) {
+          const int piece = wave * T::A_CH + i;
           int iy, ix;
           bool ok;
           if (CONV == PSO_CONV_NORMAL) {
-            iy = rc[i].oy * cv.stride + ti.kh - cv.pad;
-            ix = rc[i].ox * cv.stride + ti.kw - cv.pad;
-            ok = (unsigned)iy < (unsigned)cv.H && (unsigned)ix < (unsigned)cv.W;
+            iy = rc[i].oy * cvS + ti.kh - cvP;
+            ix = rc[i].ox * cvS + ti.kw - cvP;
+            ok = (unsigned)iy < (unsigned)cvH && (unsigned)ix < (unsigned)cvW;
           } else if (CONV == PSO_CONV_UP2) {
-            const int uy = rc[i].oy + ti.kh - cv.pad, ux = rc[i].ox + ti.kw - cv.pad;
-            ok = (unsigned)uy < (unsigned)(2 * cv.H) && (unsigned)ux < (unsigned)(2 * cv.W);
+            const int uy = rc[i].oy + ti.kh - cvP, ux = rc[i].ox + ti.kw - cvP;
+            ok = (unsigned)uy < (unsigned)(2 * cvH) && (unsigned)ux < (unsigned)(2 * cvW);
             iy = uy >> 1;
             ix = ux >> 1;
           } else {
-            const int ty = rc[i].oy + cv.pad - ti.kh, tx = rc[i].ox + cv.pad - ti.kw;
+            const int ty = rc[i].oy + cvP - ti.kh, tx = rc[i].ox + cvP - ti.kw;
             iy = ty >> 1;
             ix = tx >> 1;
-            ok = ty >= 0 && tx >= 0 && !(ty & 1) && !(tx & 1) && iy < cv.H && ix < cv.W;
+            ok = ty >= 0 && tx >= 0 && !(ty & 1) && !(tx & 1) && iy < cvH && ix < cvW;
           }
-          if (ok) src = ti.src + (((long)rc[i].b * cv.H + iy) * cv.W + ix) * ti.Cs + ti.c0 + lc * 8;
+          const bf16_t* src = ti.src + ((long)((rc[i].b * cvH + iy) * cvW + ix)) * ti.Cs + ti.c0 + lcA[i] * 8;
+          __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? src : zero), (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
         }
       } else {
-        const int k = k0 + lc * 8;
-        if (m0 + R < g.M && k < g.K1) src = g.a1 + (long)(m0 + R) * g.lda1 + k;
-      }
-      __builtin_amdgcn_global_load_lds(src, (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
-    }
 #pragma unroll
-    for (int i = 0; i < T::B_CH; ++i) {
-      const int piece = wave * T::B_CH + i;
-      const int R = piece * 8 + prow;
-      const int lc = pch ^ (R & 7);
-      const int k = k0 + lc * 8;
-      const void* src = zero;
-      if (second) {
-        if (n0 + R < g.N && k < g.K2) src = g.b2 + (long)(n0 + R) * g.ldb2 + k;
-      } else {
-        if (n0 + R < g.N && k < g.K1) src = g.b1 + (long)(n0 + R) * g.ldb1 + k;
+        for (int i = 0; i < T::A_CH; ++i) {
+          const int piece = wave * T::A_CH + i;
+          const bool ok = full || k0 + lcA[i] * 8 < K1;
+          __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? a1 + offA[i] + k0 : zero), (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
+        }
       }
-      __builtin_amdgcn_global_load_lds(src, (lds_void*)(lb + piece * 8 * BK), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < T::B_CH; ++i) {
+        const int piece = wave * T::B_CH + i;
+        const bool ok = full || k0 + lcB[i] * 8 < K1;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? b1 + offB[i] + k0 : zero), (lds_void*)(lb + piece * 8 * BK), 16, 0, 0);
+      }
+    } else {  // LoRA / second-operand K-tail (rare: one or two tiles per launch)
+      const int k0 = (t - nt1) * BK;
+#pragma unroll
+      for (int i = 0; i < T::A_CH; ++i) {
+        const int piece = wave * T::A_CH + i;
+        const int R = piece * 8 + prow;
+        const int m = min(m0 + R, g.M - 1);
+        const int k = k0 + lcA[i] * 8;
+        const bf16_t* src = g.a2 + a2_off + (long)m * g.lda2 + k;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(k < g.K2 ? src : zero), (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < T::B_CH; ++i) {
+        const int piece = wave * T::B_CH + i;
+        const int R = piece * 8 + prow;
+        const int n = min(n0 + R, g.N - 1);
+        const int k = k0 + lcB[i] * 8;
+        const bf16_t* src = g.b2 + (long)n * g.ldb2 + k;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(k < g.K2 ? src : zero), (lds_void*)(lb + piece * 8 * BK), 16, 0, 0);
+      }
     }
   };
 
@@ -246,6 +279,59 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int fr = lane & 15, fk = lane >> 4;
+  if constexpr (PIPE) {
+    // Register-pipelined schedule (2 LDS buffers + fragments of the next K-half in registers):
+    //   iteration t:  ds_read kk=1 of tile t | MFMA kk=0 of t | lgkmcnt(0), vmcnt(0) [tile t+1 landed], s_barrier |
+    //                 glds tile t+2 -> buffer of t | ds_read kk=0 of t+1 | MFMA kk=1 of t
+    // so LDS reads always overlap MFMAs and the barrier is the only cross-wave sync per K-tile.  WAR: buffer t is
+    // re-staged only after every wave retired its reads of it (lgkmcnt(0) before the barrier).  RAW: tile t+1 is
+    // read only after every wave's glds of it retired (vmcnt(0) before the same barrier).
+    static_assert(STAGES == 2, "pipelined schedule uses two LDS buffers");
+    bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+    auto read_frags = [&](int buf, int kk, bf16x8* fa, bf16x8* fb) {
+      const bf16_t* la = stage_ptr(buf);
+      const bf16_t* lb = stage_ptr(buf) + BM * BK;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / WM) + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / WN) + j * 16 + fr, kk * 4 + fk));
+    };
+    auto mfma_all = [&](const bf16x8* fa, const bf16x8* fb) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    if (nt > 0) issue_tile(0, 0);
+    if (nt > 1) issue_tile(1, 1);
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (nt > 0) read_frags(0, 0, fa0, fb0);
+    PSO_S_WAITCNT(0xC07F);  // same state on both loop-header edges (see the end of the loop body)
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      read_frags(cur, 1, fa1, fb1);
+      mfma_all(fa0, fb0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < nt) issue_tile(t + 2, cur);
+      read_frags(cur ^ 1, 0, fa0, fb0);  // unconditional (past the last tile it reads a dead buffer, never used)
+      // kk=1 fragments landed; the MI+NJ kk=0 reads just issued stay in flight behind these MFMAs
+      static_assert(MI + NJ <= 15, "lgkmcnt field");
+      PSO_S_WAITCNT(0xC07F | ((MI + NJ) << 8));
+      mfma_all(fa1, fb1);
+      // retire the kk=0 fragment reads HERE (behind the MFMAs) with a waitcnt the compiler can see, so the next
+      // iteration's MFMAs on them do not wait for the kk=1 reads issued just before (LDS returns in order, but the
+      // waitcnt pass merges the loop back-edge conservatively).  0xC07F = vmcnt(63) expcnt(7) lgkmcnt(0).
+      PSO_S_WAITCNT(0xC07F);
+    }
+  } else {
   // prologue: K-tiles 0 .. STAGES-2 in flight; wait for tile 0
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -253,7 +339,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   if (STAGES == 3 && nt > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PIECES) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
-  const int fr = lane & 15, fk = lane >> 4;
   int cur = 0;
   for (int t = 0; t < nt; ++t) {
     const bool ahead = t + STAGES - 1 < nt;
@@ -281,6 +366,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     cur = (cur + 1 == STAGES) ? 0 : cur + 1;
   }
+  }  // !PIPE
 
   // ---- epilogue: lane holds out[m][n0..n0+3] for each (i, j) ----
 #pragma unroll
@@ -341,7 +427,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   }
 }
 
-template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2>
+template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2, bool PIPE = false>
 static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   dim3 grid(nblk, ksplit);
@@ -349,23 +435,23 @@ static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
   static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
   switch (g.conv.mode) {
     case PSO_CONV_NORMAL:
-      gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES><<<grid, threads, shm, st>>>(g);
+      gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g);
       break;
-    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES><<<grid, threads, shm, st>>>(g); break;
-    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES><<<grid, threads, shm, st>>>(g); break;
-    default: gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES><<<grid, threads, shm, st>>>(g);
+    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g); break;
+    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g); break;
+    default: gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g);
   }
   return pso_check_launch("pso_gemm");
 }
@@ -412,6 +498,11 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g_gemm_variant == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
   if (g_gemm_variant == 2 && !bn64_only) return launch<128, 128, 2, 2, 3>(g, st);
   if (g_gemm_variant == 3 && !bn64_only) return launch<128, 128>(g, st);
+  if (g_gemm_variant == 6 && !bn64_only) return launch<64, 128>(g, st);
+  if (g_gemm_variant == 7 && bn256_ok) return launch<128, 256, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 8 && !bn64_only) return launch<128, 128, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 10 && bn256_ok) return launch<256, 256, 2, 4, 2, true>(g, st);
+  if (g_gemm_variant == 11 && !bn64_only) return launch<128, 128, 2, 4, 2, true>(g, st);
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).
@@ -419,10 +510,13 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.N <= 64) return launch<64, 64>(g, st);
   if (bn64_only) return tiles(128, 64) >= 512 ? launch<128, 64>(g, st) : launch<64, 64>(g, st);
   if (g.M <= 64) return launch<64, 128>(g, st);
-  // 256x256 block tile, 8 waves x (128x64): twice the MFMAs per LDS fragment read; wins once the grid covers most of
-  // the 256 CUs (one 128 KiB-LDS block per CU).
-  if (bn256_ok && tiles(256, 256) >= 180) return launch<256, 256, 2, 4, 2>(g, st);
-  if (tiles(128, 128) >= 1024) return launch<128, 128>(g, st);
+  // 256x256 block tile, 8 waves x (128x64): twice the MFMAs per LDS fragment read; wins once the grid covers the 256
+  // CUs (one 128 KiB-LDS block per CU) and N has no partial 256-column tile; implicit-GEMM convs (long K) already
+  // at half a wave of blocks.  Otherwise 128x128 with 8 waves (64x32 each).  Measured on the UNet shapes at 8 images
+  // (tools/gemm_bench.py): e.g. L2 qkv 8192x3840x1280 713 vs 645 TF/s; L2 proj 8192x1280x1280 531 vs 474.
+  if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= (g.conv.mode ? 128 : 256))
+    return launch<256, 256, 2, 4, 2>(g, st);
+  if (tiles(128, 128) >= 256) return launch<128, 128, 2, 4, 2>(g, st);
   if (tiles(64, 128) >= 512) return (g.N % 128 == 0) ? launch<64, 128>(g, st) : launch<128, 64>(g, st);
   return launch<64, 64>(g, st);
 }
@@ -553,6 +647,8 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
   PSO_ARG_CHECK(!a2 || (b2 && (K2 % 8) == 0 && al16(a2) && al16(b2) && (lda2 % 8) == 0 && (ldb2 % 8) == 0),
                 "pso_gemm: bad second operand");
   PSO_ARG_CHECK(out_dtype == PSO_BF16 || out_dtype == PSO_F32, "pso_gemm: bad out dtype");
+  PSO_ARG_CHECK((long)M * lda1 < 0x7fffffffL && (long)N * ldb1 < 0x7fffffffL,
+                "pso_gemm: operand spans more than 2^31 elements");
   PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_gemm: accumulate needs f32 output");
   PSO_ARG_CHECK(!rowbias || rows_per_group > 0, "pso_gemm: rowbias needs rows_per_group > 0");
   GemmArgs g{};

@@ -30,21 +30,23 @@ def main():
 
 def run(dev):
     rows = []
-    for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (16384, 5120, 640, "L1 ff.proj"),
-                             (16384, 640, 2560, "L1 ff.out"), (16384, 1920, 640, "L1 qkv"),
-                             (16384, 640, 640, "L1 out/proj"), (4096, 10240, 1280, "L2 ff.proj"),
-                             (4096, 1280, 5120, "L2 ff.out"), (4096, 3840, 1280, "L2 qkv"),
-                             (4096, 1280, 1280, "L2 proj"), (4096, 96, 1280, "L2 lora u qkv"),
-                             (4096, 32, 1280, "L2 lora v"), (16384, 32, 640, "L1 lora v")]:
+    Bi = int(os.environ.get("GEMM_IMAGES", "8"))
+    L1, L2 = 4096 * Bi, 1024 * Bi
+    for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (L1, 5120, 640, "L1 ff.proj"),
+                             (L1, 640, 2560, "L1 ff.out"), (L1, 1920, 640, "L1 qkv"),
+                             (L1, 640, 640, "L1 out/proj"), (L2, 10240, 1280, "L2 ff.proj"),
+                             (L2, 1280, 5120, "L2 ff.out"), (L2, 3840, 1280, "L2 qkv"),
+                             (L2, 1280, 1280, "L2 proj"), (L2, 1280, 10240, "L2 geglu dX"),
+                             (L2, 5120, 1280, "L2 ff.out dX")]:
         a = torch.randn(M, Kd, device=dev).bfloat16()
         w = torch.randn(N, Kd, device=dev).bfloat16()
         ms = t_ms(lambda: K.gemm(a, w))
         rows.append((name, f"{M}x{N}x{Kd}", ms, 2 * M * N * Kd / ms / 1e9))
-    for (B, H, Ci, Co, name, mode) in [(4, 128, 320, 320, "L0 conv 320", K.CONV_NORMAL),
-                                       (4, 64, 640, 640, "L1 conv 640", K.CONV_NORMAL),
-                                       (4, 32, 1280, 1280, "L2 conv 1280", K.CONV_NORMAL),
-                                       (4, 32, 2560, 1280, "L2 conv 2560->1280", K.CONV_NORMAL),
-                                       (4, 64, 1280, 1280, "up conv 1280 @64->128", K.CONV_UP2)]:
+    for (B, H, Ci, Co, name, mode) in [(Bi, 128, 320, 320, "L0 conv 320", K.CONV_NORMAL),
+                                       (Bi, 64, 640, 640, "L1 conv 640", K.CONV_NORMAL),
+                                       (Bi, 32, 1280, 1280, "L2 conv 1280", K.CONV_NORMAL),
+                                       (Bi, 32, 2560, 1280, "L2 conv 2560->1280", K.CONV_NORMAL),
+                                       (Bi, 64, 1280, 1280, "up conv 1280 @64->128", K.CONV_UP2)]:
         x = torch.randn(B, H, H, Ci, device=dev).bfloat16()
         w = torch.randn(Co, 3, 3, Ci, device=dev).bfloat16()
         Ho = 2 * H if mode == K.CONV_UP2 else H
