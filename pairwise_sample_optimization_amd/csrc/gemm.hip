@@ -503,6 +503,14 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g_gemm_variant == 8 && !bn64_only) return launch<128, 128, 2, 4, 2>(g, st);
   if (g_gemm_variant == 10 && bn256_ok) return launch<256, 256, 2, 4, 2, true>(g, st);
   if (g_gemm_variant == 11 && !bn64_only) return launch<128, 128, 2, 4, 2, true>(g, st);
+  const bool n160 = (g.N % 160) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
+  const bool n320 = (g.N % 320) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
+  if (g_gemm_variant == 12 && n160) return launch<128, 160, 2, 2, 2>(g, st);
+  if (g_gemm_variant == 14 && n160) return launch<256, 160, 2, 2, 2>(g, st);
+  if (g_gemm_variant == 16 && n160) return launch<256, 160, 2, 2, 2, true>(g, st);
+  if (g_gemm_variant == 17 && n320) return launch<128, 320, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 18 && n320) return launch<256, 320, 2, 4, 2>(g, st);
+  if (g_gemm_variant == 19 && n160) return launch<128, 160, 2, 2, 2, true>(g, st);
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).
@@ -514,6 +522,13 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // CUs (one 128 KiB-LDS block per CU) and N has no partial 256-column tile; implicit-GEMM convs (long K) already
   // at half a wave of blocks.  Otherwise 128x128 with 8 waves (64x32 each).  Measured on the UNet shapes at 8 images
   // (tools/gemm_bench.py): e.g. L2 qkv 8192x3840x1280 713 vs 645 TF/s; L2 proj 8192x1280x1280 531 vs 474.
+  // Very large grids (>= 4 rounds of 256x256 tiles: L1/L2 ff.proj, the 128^2 upsample conv) keep 256x256.  Otherwise
+  // N % 160 == 0 (every SDXL width: 320 | N) takes 128x160 with 4 waves of 64x80: fewer LDS bytes per MFMA than the
+  // 8-wave 128x128 (64x32 wave tiles) and tile counts that divide the 512 co-resident slots (M=8192, N=1280 -> 512
+  // tiles).  tools/gemm_bench.py at 8 images: L2 ff.out 8192x1280x5120 797 -> 1097 TF/s, L2 proj 636 -> 816,
+  // L0/L1/L2 3x3 convs 733/887/795 -> 921/994/1005.
+  if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= 1024) return launch<256, 256, 2, 4, 2>(g, st);
+  if (n160 && tiles(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
   if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= (g.conv.mode ? 128 : 256))
     return launch<256, 256, 2, 4, 2>(g, st);
   if (tiles(128, 128) >= 256) return launch<128, 128, 2, 4, 2>(g, st);

@@ -31,17 +31,22 @@ def main():
 def run(dev):
     rows = []
     Bi = int(os.environ.get("GEMM_IMAGES", "8"))
+    if os.environ.get("GEMM_ONLY_LINEAR"):
+        pass
     L1, L2 = 4096 * Bi, 1024 * Bi
     for (M, N, Kd, name) in [(4096, 4096, 4096, "square"), (L1, 5120, 640, "L1 ff.proj"),
                              (L1, 640, 2560, "L1 ff.out"), (L1, 1920, 640, "L1 qkv"),
                              (L1, 640, 640, "L1 out/proj"), (L2, 10240, 1280, "L2 ff.proj"),
                              (L2, 1280, 5120, "L2 ff.out"), (L2, 3840, 1280, "L2 qkv"),
                              (L2, 1280, 1280, "L2 proj"), (L2, 1280, 10240, "L2 geglu dX"),
+                             (2 * L2, 1280, 5120, "L2x2 ff.out"), (2 * L2, 1280, 1280, "L2x2 proj"),
                              (L2, 5120, 1280, "L2 ff.out dX")]:
         a = torch.randn(M, Kd, device=dev).bfloat16()
         w = torch.randn(N, Kd, device=dev).bfloat16()
         ms = t_ms(lambda: K.gemm(a, w))
-        rows.append((name, f"{M}x{N}x{Kd}", ms, 2 * M * N * Kd / ms / 1e9))
+        ref = a.float() @ w.float().t()
+        err = ((K.gemm(a, w).float() - ref).norm() / ref.norm()).item()
+        rows.append((name, f"{M}x{N}x{Kd} e={err:.1e}", ms, 2 * M * N * Kd / ms / 1e9))
     for (B, H, Ci, Co, name, mode) in [(Bi, 128, 320, 320, "L0 conv 320", K.CONV_NORMAL),
                                        (Bi, 64, 640, 640, "L1 conv 640", K.CONV_NORMAL),
                                        (Bi, 32, 1280, 1280, "L2 conv 1280", K.CONV_NORMAL),
