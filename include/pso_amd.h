@@ -105,6 +105,8 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
 void pso_gemm_set_variant(int v);
 /* Benchmark knob: split count of pso_gemm_tn over the reduction rows (0 = automatic). */
 void pso_gemm_tn_set_split(int ks);
+/* benchmark knob: attention forward tile (0 = auto, 2 = 128 / 4 = 256 queries per workgroup) */
+void pso_attention_set_variant(int v);
 
 /* TN GEMM, f32 accumulate: out[I][J] += alpha * sum_m A[m][I] * B[m][J] (A [M][I], B [M][J] row-major, row strides
  * lda/ldb; I, J multiples of 8).  Replaces the peft LoRA weight-gradient GEMMs of the backward (dA = v^T x,

@@ -40,6 +40,7 @@ SIGNATURES = {
                       ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
     "pso_gemm_tn_set_split": (None, [ci]),
+    "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),

@@ -65,6 +65,7 @@ struct AttnArgs {
   bf16_t *dq, *dk, *dv; long lddq, lddk, lddv; long sdq_b, sdk_b, sdv_b;
   float *dk_acc, *dv_acc;      // fp32 [B][Sk][H*64] when q is split (cross-attention)
   int q_split;
+  int nbatch;                  // B (split-slice stride)
 };
 
 // stage a [64 rows][64 d] bf16 tile (rows r0.. of a [S][ld] matrix, zero beyond nrows) into registers: 2 chunks/thread
@@ -90,56 +91,102 @@ __device__ __forceinline__ void stage_store(const uint4 (&r)[2], bf16_t* img, in
 // ================================================================================================================
 // forward
 // ================================================================================================================
-__global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sK[2][ATT_KT * ATT_D];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[2][ATT_KT * ATT_D];
+// Cross-lane max over the 4 lanes {c, c+16, c+32, c+48} that hold one query row (v_permlane16/32_swap: VALU, no LDS).
+__device__ __forceinline__ float rowmax4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float rowsum4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+typedef __attribute__((address_space(3))) void att_lds_void;
+
+// XCD-aware flat block order: the hardware deals blocks round-robin over the 8 XCDs; give each XCD a contiguous run of
+// logical blocks so the query blocks of one (batch, head) share one L2 copy of its K/V.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  if (nblk < 8) return bid;
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// One workgroup = 4 waves x (16*QI) query rows of one (batch, head).  K/V tiles of 64 keys go global -> LDS directly
+// (global_load_lds_dwordx4, 2 K + 2 V pieces of 8 rows x 128 B per wave per tile) through a 3-stage ring, two tiles in
+// flight behind a counted vmcnt and ONE s_barrier per tile.  The LDS swizzles are applied on the source side (lane i of
+// a piece lands at byte 16*i): K row-image chunk p ^ (row & 7), V transposed-read chunk p ^ 2*((row >> 1) & 3).
+// Softmax: raw-score running max (exp2(s*c - m*c) = one FMA + one exp per score), per-lane partial row sums reduced
+// once at the end, the O/l rescale skipped when no row max moved (wave-uniform), key masking on the last tile only.
+template <int QI>
+__global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, int nqb) {
+  constexpr int STG = 3;
+  constexpr int PIECES = 4;  // glds per wave per tile
+  __shared__ __attribute__((aligned(16))) bf16_t sKV[STG][2][ATT_KT * ATT_D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb, bh = bid / nqb;
+  const int h = bh % a.H, b = bh / a.H;
+  const int q0 = qb * (64 * QI) + wave * (16 * QI);
 
   const bf16_t* Q = a.q + b * a.sq_b + h * ATT_D;
   const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
   const bf16_t* V = a.v + b * a.sv_b + h * ATT_D;
+  const float c2 = a.scale_log2;
+
+  // this lane's staging source rows/chunks: piece pw (0/1) of wave w covers tile rows (2w + pw)*8 .. +8
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcK = pch ^ prow;
+  const int lcV = pch ^ (2 * ((prow >> 1) & 3));
+  const int nkt = (a.Sk + ATT_KT - 1) / ATT_KT;
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int pw = 0; pw < 2; ++pw) {
+      const int piece = wave * 2 + pw;
+      const int key = min(kt * ATT_KT + piece * 8 + prow, a.Sk - 1);  // clamped rows are masked (p = 0)
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(K + (long)key * a.ldk + lcK * 8),
+                                       (att_lds_void*)(sKV[buf][0] + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(V + (long)key * a.ldv + lcV * 8),
+                                       (att_lds_void*)(sKV[buf][1] + piece * 8 * ATT_D), 16, 0, 0);
+    }
+  };
 
   // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q0 + qi*16 + c][ds*32 + 8g .. +8]
-  bf16x8 qf[2][2];
+  bf16x8 qf[QI][2];
 #pragma unroll
-  for (int qi = 0; qi < 2; ++qi) {
-    const int qr = q0 + qi * 16 + c;
+  for (int qi = 0; qi < QI; ++qi) {
+    const int qr = min(q0 + qi * 16 + c, a.Sq - 1);
 #pragma unroll
-    for (int ds = 0; ds < 2; ++ds) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (qr < a.Sq) v = *reinterpret_cast<const uint4*>(Q + (long)qr * a.ldq + ds * 32 + 8 * g);
-      qf[qi][ds] = __builtin_bit_cast(bf16x8, v);
-    }
+    for (int ds = 0; ds < 2; ++ds)
+      qf[qi][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Q + (long)qr * a.ldq + ds * 32 + 8 * g));
   }
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
 
-  f32x4 o[2][4];
+  f32x4 o[QI][4];
+  float m_run[QI], l_run[QI];
 #pragma unroll
-  for (int qi = 0; qi < 2; ++qi)
+  for (int qi = 0; qi < QI; ++qi) {
+    m_run[qi] = -INFINITY;
+    l_run[qi] = 0.f;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[qi][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
-
-  const int nkt = (a.Sk + ATT_KT - 1) / ATT_KT;
-  uint4 rk[2], rv[2];
-  stage_load(rk, K, a.ldk, 0, a.Sk, tid);
-  stage_load(rv, V, a.ldv, 0, a.Sk, tid);
-  stage_store<false>(rk, sK[0], tid);
-  stage_store<true>(rv, sV[0], tid);
-  __syncthreads();
+  }
 
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) {
-      stage_load(rk, K, a.ldk, (kt + 1) * ATT_KT, a.Sk, tid);
-      stage_load(rv, V, a.ldv, (kt + 1) * ATT_KT, a.Sk, tid);
-    }
-    const bf16_t* k_img = sK[cur];
-    const bf16_t* v_img = sV[cur];
-    // ---- S^T tiles: s[qi][kj] holds S[q = qi*16 + c][key = kj*16 + 4g + r] ----
-    f32x4 s[2][4];
+    // tile kt landed (this wave's pieces: all but the PIECES youngest), then every wave's (barrier); the barrier also
+    // orders every wave's reads of tile kt-1 before the re-staging of its buffer below
+    if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % STG);
+    const bf16_t* k_img = sKV[kt % STG][0];
+    const bf16_t* v_img = sKV[kt % STG][1];
+    // ---- S^T tiles: s[qi][kj] holds S[q = qi*16 + c][key = kj*16 + 4g + r] (raw scores) ----
+    f32x4 s[QI][4];
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {
       bf16x8 kf[2];
@@ -147,84 +194,83 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a) {
       for (int ds = 0; ds < 2; ++ds)
         kf[ds] = *reinterpret_cast<const bf16x8*>(k_img + swz_row(kj * 16 + c, ds * 4 + g));
 #pragma unroll
-      for (int qi = 0; qi < 2; ++qi) {
+      for (int qi = 0; qi < QI; ++qi) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qi][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qi][1], acc, 0, 0, 0);
-        s[qi][kj] = acc;
+        s[qi][kj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qi][1], acc, 0, 0, 0);
       }
     }
-    // ---- online softmax (base 2) ----
     const int kbase = kt * ATT_KT;
+    if (kbase + ATT_KT > a.Sk) {  // partial last tile (wave-uniform)
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
-      float mx = -INFINITY;
+      for (int qi = 0; qi < QI; ++qi)
 #pragma unroll
-      for (int kj = 0; kj < 4; ++kj)
+        for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kbase + kj * 16 + 4 * g + r;
-          float x = s[qi][kj][r] * a.scale_log2;
-          if (key >= a.Sk) x = -INFINITY;
-          s[qi][kj][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          for (int r = 0; r < 4; ++r)
+            if (kbase + kj * 16 + 4 * g + r >= a.Sk) s[qi][kj][r] = -INFINITY;
+    }
+    // ---- online softmax (base 2, raw-score max) ----
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) {
+      float mx = fmaxf(fmaxf(s[qi][0][0], s[qi][0][1]), fmaxf(s[qi][0][2], s[qi][0][3]));
+#pragma unroll
+      for (int kj = 1; kj < 4; ++kj)
+        mx = fmaxf(mx, fmaxf(fmaxf(s[qi][kj][0], s[qi][kj][1]), fmaxf(s[qi][kj][2], s[qi][kj][3])));
+      mx = rowmax4(mx);
       const float m_new = fmaxf(m_run[qi], mx);
-      const float alpha = exp2f(m_run[qi] - m_new);
+      if (__any(m_new > m_run[qi])) {
+        const float alpha = fast_exp2((m_run[qi] - m_new) * c2);  // first tile: exp2(-inf) = 0
+        l_run[qi] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qi][dt] *= alpha;
+        m_run[qi] = m_new;
+      }
+      const float mc = m_run[qi] * c2;
       float sum = 0.f;
 #pragma unroll
       for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[qi][kj][r] - m_new);
+          const float p = fast_exp2(fmaf(s[qi][kj][r], c2, -mc));
           s[qi][kj][r] = p;
           sum += p;
         }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      l_run[qi] = l_run[qi] * alpha + sum;
-      m_run[qi] = m_new;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[qi][dt] *= alpha;
+      l_run[qi] += sum;  // this lane's keys only; the 4 lanes of a row are summed in the epilogue
     }
     // ---- O^T += V^T . P^T ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pf[2];
+      bf16x8 pf[QI];
 #pragma unroll
-      for (int qi = 0; qi < 2; ++qi) pf[qi] = pack_p(s[qi][2 * ks], s[qi][2 * ks + 1]);
+      for (int qi = 0; qi < QI; ++qi) pf[qi] = pack_p(s[qi][2 * ks], s[qi][2 * ks + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const s16x4 v0 = tr_read(v_img, (2 * ks) * 16 + 4 * g, dt * 16, lane);
         const s16x4 v1 = tr_read(v_img, (2 * ks + 1) * 16 + 4 * g, dt * 16, lane);
         const bf16x8 vf = cat_frag(v0, v1);
 #pragma unroll
-        for (int qi = 0; qi < 2; ++qi) o[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qi], o[qi][dt], 0, 0, 0);
+        for (int qi = 0; qi < QI; ++qi) o[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qi], o[qi][dt], 0, 0, 0);
       }
     }
-    if (kt + 1 < nkt) {
-      stage_store<false>(rk, sK[cur ^ 1], tid);
-      stage_store<true>(rv, sV[cur ^ 1], tid);
-    }
-    __syncthreads();
   }
 
   // ---- epilogue: lane holds O[q = qi*16 + c][d = dt*16 + 4g + r] ----
   bf16_t* O = a.o + b * a.so_b + h * ATT_D;
 #pragma unroll
-  for (int qi = 0; qi < 2; ++qi) {
+  for (int qi = 0; qi < QI; ++qi) {
+    const float l = rowsum4(l_run[qi]);
     const int qr = q0 + qi * 16 + c;
     if (qr >= a.Sq) continue;
-    const float inv = 1.f / l_run[qi];
+    const float inv = 1.f / l;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const f32x4 v = o[qi][dt];
       *reinterpret_cast<uint2*>(O + (long)qr * a.ldo + dt * 16 + 4 * g) =
           make_uint2(pack2bf(v[0] * inv, v[1] * inv), pack2bf(v[2] * inv, v[3] * inv));
     }
-    if (a.lse && g == 0) a.lse[((long)b * a.H + h) * a.Sq + qr] = (m_run[qi] + log2f(l_run[qi])) * 0.69314718055994531f;
+    if (a.lse && g == 0)
+      a.lse[((long)b * a.H + h) * a.Sq + qr] = (m_run[qi] * c2 + log2f(l)) * 0.69314718055994531f;
   }
 }
 
@@ -259,21 +305,28 @@ __global__ void attn_delta_kernel(AttnArgs a, int B) {
 }
 
 // ================================================================================================================
-// backward dK/dV: one workgroup = 128 keys of one (b, h) (32 per wave, keys on the MFMA lane axis); loops over the
-// query tiles [qa, qb).  Scores S[q][k] = Q.K^T with Q fragments as the A operand -> lane holds S[q=4g+r][k=c].
+// backward dK/dV: one workgroup = 4 waves x (16*KJ) keys of one (b, h) (keys on the MFMA lane axis); query tiles of
+// 64 stream through a STG-stage LDS ring filled directly from global memory: per tile the Q row image, the Q
+// transposed-read image, the dO row image, the dO transposed-read image (8 pieces of 8 rows x 128 B each, 8 per wave)
+// and the 64 LSE / delta values (one 256-B dword piece each, waves 0 / 1).  Scores S[q][k] = Q.K^T with Q fragments
+// as the A operand -> lane holds S[q = 4g + r][k = c]; P and dS then feed dV^T += dO^T P and dK^T += Q^T dS as
+// lane-local B operands (query order permuted inside each 32-deep step, matching the transposed dO / Q reads).
 // ================================================================================================================
-__global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sQr[ATT_KT * ATT_D];   // row image of the Q tile
-  __shared__ __attribute__((aligned(16))) bf16_t sQt[ATT_KT * ATT_D];   // transposed-read image
-  __shared__ __attribute__((aligned(16))) bf16_t sOr[ATT_KT * ATT_D];   // dO row image
-  __shared__ __attribute__((aligned(16))) bf16_t sOt[ATT_KT * ATT_D];   // dO transposed-read image
-  __shared__ float sL[ATT_KT], sD[ATT_KT];
+template <int KJ, int STG>
+__global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a, int nkb) {
+  constexpr int IMG = ATT_KT * ATT_D;  // elements of one 64 x 64 image
+  constexpr int PIECES = 8;            // 16-B glds per wave per tile (+1 dword piece on waves 0 and 1)
+  extern __shared__ __attribute__((aligned(16))) bf16_t att_dyn[];
+  bf16_t* const sbase = att_dyn;                                   // [STG][4][IMG]: Qr, Qt, Or, Ot
+  float* const sLD = reinterpret_cast<float*>(att_dyn + STG * 4 * IMG);  // [STG][2][64]: LSE, delta
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const int nkb = (a.Sk + 127) / 128;
-  const int kb = blockIdx.x % nkb, split = blockIdx.x / nkb;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int k0 = kb * 128 + wave * 32;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_bh = nkb * a.q_split;
+  const int bh = bid / per_bh, rem = bid - bh * per_bh;
+  const int split = rem / nkb, kb = rem - split * nkb;
+  const int h = bh % a.H, b = bh / a.H;
+  const int k0 = kb * (64 * KJ) + wave * (16 * KJ);
 
   const bf16_t* Q = a.q + b * a.sq_b + h * ATT_D;
   const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
@@ -281,85 +334,108 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dkv_kernel(AttnArgs a
   const bf16_t* DO = a.dO + b * a.sdo_b + h * ATT_D;
   const float* LSE = a.lse + ((long)b * a.H + h) * a.Sq;
   const float* DEL = a.delta + ((long)b * a.H + h) * a.Sq;
-
-  // K and V fragments of this wave's 32 keys (B operands): lane holds K[k0 + kj*16 + c][ds*32 + 8g ..]
-  bf16x8 kf[2][2], vf[2][2];
-#pragma unroll
-  for (int kj = 0; kj < 2; ++kj) {
-    const int kr = k0 + kj * 16 + c;
-#pragma unroll
-    for (int ds = 0; ds < 2; ++ds) {
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (kr < a.Sk) {
-        kv = *reinterpret_cast<const uint4*>(K + (long)kr * a.ldk + ds * 32 + 8 * g);
-        vv = *reinterpret_cast<const uint4*>(V + (long)kr * a.ldv + ds * 32 + 8 * g);
-      }
-      kf[kj][ds] = __builtin_bit_cast(bf16x8, kv);
-      vf[kj][ds] = __builtin_bit_cast(bf16x8, vv);
-    }
-  }
-  f32x4 dk[2][4], dv[2][4];  // [kj][dt]: lane holds d?[k = kj*16 + c][d = dt*16 + 4g + r]
-#pragma unroll
-  for (int kj = 0; kj < 2; ++kj)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dk[kj][dt] = dv[kj][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float ln2inv = 1.4426950408889634f;
+  const float c2 = a.scale_log2;
 
   const int nqt = (a.Sq + ATT_KT - 1) / ATT_KT;
   const int per = (nqt + a.q_split - 1) / a.q_split;
   const int qa = split * per, qb = min(nqt, qa + per);
-  const float ln2inv = 1.4426950408889634f;
+  const int n = qb > qa ? qb - qa : 0;
 
-  for (int qt = qa; qt < qb; ++qt) {
-    const int qbase = qt * ATT_KT;
-    uint4 rq[2], ro[2];
-    stage_load(rq, Q, a.ldq, qbase, a.Sq, tid);
-    stage_load(ro, DO, a.lddo, qbase, a.Sq, tid);
-    __syncthreads();  // previous tile fully consumed
-    stage_store<false>(rq, sQr, tid);
-    stage_store<true>(rq, sQt, tid);
-    stage_store<false>(ro, sOr, tid);
-    stage_store<true>(ro, sOt, tid);
-    if (tid < ATT_KT) {
-      const int q = qbase + tid;
-      sL[tid] = q < a.Sq ? LSE[q] * ln2inv : INFINITY;  // base-2 LSE; padded rows give p = 0
-      sD[tid] = q < a.Sq ? DEL[q] : 0.f;
+  // staging: wave w fills rows (2w + pw)*8 .. +8 of each of the four images
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcR = pch ^ prow;                       // row-image source chunk
+  const int lcT = pch ^ (2 * ((prow >> 1) & 3));    // transposed-image source chunk
+  auto issue = [&](int qt, int buf) {
+    bf16_t* img = sbase + buf * 4 * IMG;
+    if (wave < 2) {  // LSE (wave 0) / delta (wave 1): one dword per lane, issued first so it retires first
+      const int q = min(qt * ATT_KT + lane, a.Sq - 1);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>((wave == 0 ? LSE : DEL) + q),
+                                       (att_lds_void*)(sLD + (buf * 2 + wave) * 64), 4, 0, 0);
     }
-    __syncthreads();
-    // S and dP for 4 q-subtiles x 2 key subtiles: lane holds X[q = qs*16 + 4g + r][k = kj*16 + c]
-    f32x4 p[4][2], ds_[4][2];
 #pragma unroll
-    for (int qs = 0; qs < 4; ++qs) {
-      bf16x8 qa_[2], oa_[2];
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2) {
-        qa_[d2] = *reinterpret_cast<const bf16x8*>(sQr + swz_row(qs * 16 + c, d2 * 4 + g));
-        oa_[d2] = *reinterpret_cast<const bf16x8*>(sOr + swz_row(qs * 16 + c, d2 * 4 + g));
-      }
-      float lq[4], dq_[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        lq[r] = sL[qs * 16 + 4 * g + r];
-        dq_[r] = sD[qs * 16 + 4 * g + r];
-      }
-#pragma unroll
-      for (int kj = 0; kj < 2; ++kj) {
-        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
-        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[0], kf[kj][0], sacc, 0, 0, 0);
-        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[1], kf[kj][1], sacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[0], vf[kj][0], pacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[1], vf[kj][1], pacc, 0, 0, 0);
-        const bool kvalid = (k0 + kj * 16 + c) < a.Sk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pr = kvalid ? exp2f(sacc[r] * a.scale_log2 - lq[r]) : 0.f;
-          p[qs][kj][r] = pr;
-          ds_[qs][kj][r] = pr * (pacc[r] - dq_[r]);
-        }
-      }
+    for (int pw = 0; pw < 2; ++pw) {
+      const int piece = wave * 2 + pw;
+      const int q = min(qt * ATT_KT + piece * 8 + prow, a.Sq - 1);  // clamped rows: masked through the LSE
+      const bf16_t* qrow = Q + (long)q * a.ldq;
+      const bf16_t* orow = DO + (long)q * a.lddo;
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(qrow + lcR * 8), (att_lds_void*)(img + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(qrow + lcT * 8), (att_lds_void*)(img + IMG + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(orow + lcR * 8), (att_lds_void*)(img + 2 * IMG + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(orow + lcT * 8), (att_lds_void*)(img + 3 * IMG + piece * 8 * ATT_D), 16, 0, 0);
     }
-    // dV^T[d][k] += dO^T . P ;  dK^T[d][k] += Q^T . dS   (q permuted within 32-deep steps, lane-local B operands)
+  };
+
+  // K and V fragments of this wave's 16*KJ keys (B operands): lane holds K[k0 + kj*16 + c][ds*32 + 8g ..]
+  bf16x8 kf[KJ][2], vf[KJ][2];
+#pragma unroll
+  for (int kj = 0; kj < KJ; ++kj) {
+    const int kr = min(k0 + kj * 16 + c, a.Sk - 1);  // clamped keys: computed, never stored
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      kf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(K + (long)kr * a.ldk + ds * 32 + 8 * g));
+      vf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(V + (long)kr * a.ldv + ds * 32 + 8 * g));
+    }
+  }
+  f32x4 dk[KJ][4], dv[KJ][4];  // [kj][dt]: lane holds d?[k = kj*16 + c][d = dt*16 + 4g + r]
+#pragma unroll
+  for (int kj = 0; kj < KJ; ++kj)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[kj][dt] = dv[kj][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (n > 0) issue(qa, 0);
+  if (STG == 3 && n > 1) issue(qa + 1, 1);
+  for (int i = 0; i < n; ++i) {
+    if (STG == 3 && i + 1 < n) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (i + STG - 1 < n) issue(qa + i + STG - 1, (i + STG - 1) % STG);
+    const int buf = i % STG;
+    const bf16_t* sQr = sbase + buf * 4 * IMG;
+    const bf16_t* sQt = sQr + IMG;
+    const bf16_t* sOr = sQr + 2 * IMG;
+    const bf16_t* sOt = sQr + 3 * IMG;
+    const float* sL = sLD + buf * 2 * 64;
+    const float* sD = sL + 64;
+    const int qbase = (qa + i) * ATT_KT;
+    const bool qpart = qbase + ATT_KT > a.Sq;
 #pragma unroll
     for (int qk = 0; qk < 2; ++qk) {
+      // P and dS for 32 queries (2 subtiles) x this wave's keys: lane holds X[q = qs*16 + 4g + r][k = kj*16 + c]
+      f32x4 p[2][KJ], dsv[2][KJ];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const int qs = 2 * qk + qh;
+        bf16x8 qa_[2], oa_[2];
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          qa_[d2] = *reinterpret_cast<const bf16x8*>(sQr + swz_row(qs * 16 + c, d2 * 4 + g));
+          oa_[d2] = *reinterpret_cast<const bf16x8*>(sOr + swz_row(qs * 16 + c, d2 * 4 + g));
+        }
+        const float4 l4 = *reinterpret_cast<const float4*>(sL + qs * 16 + 4 * g);
+        const float4 d4 = *reinterpret_cast<const float4*>(sD + qs * 16 + 4 * g);
+        float lq[4] = {l4.x * ln2inv, l4.y * ln2inv, l4.z * ln2inv, l4.w * ln2inv};
+        const float dq_[4] = {d4.x, d4.y, d4.z, d4.w};
+        if (qpart) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (qbase + qs * 16 + 4 * g + r >= a.Sq) lq[r] = INFINITY;  // padded query rows: p = 0
+        }
+#pragma unroll
+        for (int kj = 0; kj < KJ; ++kj) {
+          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[0], kf[kj][0], sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[1], kf[kj][1], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[0], vf[kj][0], pacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[1], vf[kj][1], pacc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = fast_exp2(fmaf(sacc[r], c2, -lq[r]));
+            p[qh][kj][r] = pr;
+            dsv[qh][kj][r] = pr * (pacc[r] - dq_[r]);
+          }
+        }
+      }
+      // dV^T[d][k] += dO^T . P ;  dK^T[d][k] += Q^T . dS
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8 of = cat_frag(tr_read(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
@@ -367,11 +443,9 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dkv_kernel(AttnArgs a
         const bf16x8 qf = cat_frag(tr_read(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
                                    tr_read(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
 #pragma unroll
-        for (int kj = 0; kj < 2; ++kj) {
-          dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pack_p(p[2 * qk][kj], p[2 * qk + 1][kj]),
-                                                              dv[kj][dt], 0, 0, 0);
-          dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, pack_p(ds_[2 * qk][kj], ds_[2 * qk + 1][kj]),
-                                                              dk[kj][dt], 0, 0, 0);
+        for (int kj = 0; kj < KJ; ++kj) {
+          dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pack_p(p[0][kj], p[1][kj]), dv[kj][dt], 0, 0, 0);
+          dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, pack_p(dsv[0][kj], dsv[1][kj]), dk[kj][dt], 0, 0, 0);
         }
       }
     }
@@ -379,20 +453,19 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dkv_kernel(AttnArgs a
   // ---- epilogue: lane holds d?[k = k0 + kj*16 + c][d = dt*16 + 4g + r]; dK carries the softmax scale ----
   const float sc = a.scale_log2 * 0.69314718055994531f;
 #pragma unroll
-  for (int kj = 0; kj < 2; ++kj) {
+  for (int kj = 0; kj < KJ; ++kj) {
     const int kr = k0 + kj * 16 + c;
     if (kr >= a.Sk) continue;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const int d = h * ATT_D + dt * 16 + 4 * g;
-      if (a.q_split > 1) {
-        float* pk = a.dk_acc + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
-        float* pv = a.dv_acc + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          atomicAdd(pk + r, dk[kj][dt][r] * sc);
-          atomicAdd(pv + r, dv[kj][dt][r]);
-        }
+      if (a.q_split > 1) {  // this query split's partial sums -> its own fp32 slice (reduced by reduce_splits_kernel)
+        const long slice = (long)split * (a.nbatch * (long)a.Sk) * (a.H * ATT_D);
+        float* pk = a.dk_acc + slice + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
+        float* pv = a.dv_acc + slice + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
+        *reinterpret_cast<float4*>(pk) = make_float4(dk[kj][dt][0] * sc, dk[kj][dt][1] * sc, dk[kj][dt][2] * sc,
+                                                     dk[kj][dt][3] * sc);
+        *reinterpret_cast<float4*>(pv) = make_float4(dv[kj][dt][0], dv[kj][dt][1], dv[kj][dt][2], dv[kj][dt][3]);
       } else {
         *reinterpret_cast<uint2*>(a.dk + b * a.sdk_b + (long)kr * a.lddk + d) =
             make_uint2(pack2bf(dk[kj][dt][0] * sc, dk[kj][dt][1] * sc), pack2bf(dk[kj][dt][2] * sc, dk[kj][dt][3] * sc));
@@ -475,7 +548,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kbase + kj * 16 + 4 * g + r;
-          const float p = key < a.Sk ? exp2f(sacc[r] * a.scale_log2 - lq[qi]) : 0.f;
+          const float p = key < a.Sk ? fast_exp2(sacc[r] * a.scale_log2 - lq[qi]) : 0.f;
           dsT[qi][kj][r] = p * (pacc[r] - dl[qi]);
         }
       }
@@ -509,18 +582,43 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
   }
 }
 
-__global__ void f32_to_bf16_strided_kernel(long rows, int cols, const float* __restrict__ src, bf16_t* __restrict__ dst,
-                                           long ldd) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / cols;
-    const int cc = (int)(i - r * cols);
-    dst[r * ldd + cc] = f2bf(src[i]);
+// dst[r][c] = bf16( sum_s src[s][r][c] ) : the query-split partials of the cross-attention dK / dV
+__global__ void reduce_splits_kernel(long rows, int cols, int nsplit, const float* __restrict__ src, long split_stride,
+                                     bf16_t* __restrict__ dst, long ldd) {
+  const int c4 = cols / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * c4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / c4;
+    const int cc = (int)(i - r * c4) * 4;
+    float4 acc = *reinterpret_cast<const float4*>(src + r * cols + cc);
+    for (int sp = 1; sp < nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(src + sp * split_stride + r * cols + cc);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<uint2*>(dst + r * ldd + cc) = make_uint2(pack2bf(acc.x, acc.y), pack2bf(acc.z, acc.w));
   }
 }
+
+// Query splits of the dK/dV sweep when there are few key blocks (cross-attention over the 77 text tokens): enough
+// workgroups for ~2 per CU; each split writes its own fp32 partial slice (no atomics).
+static int cross_qsplit(int B, int H, int Sq, int Sk) {
+  if (Sk > 256) return 1;
+  const int nqt = cdiv(Sq, ATT_KT);
+  int qs = cdiv(512, (long)cdiv(Sk, 128) * H * B);
+  if (qs > nqt) qs = nqt;
+  return qs < 1 ? 1 : qs;
+}
+
+static int g_attn_fwd_variant = 0;
+static int g_attn_bwd_variant = 0;  // benchmark knob: 0 auto, 2 / 4 = keys per wave / 16  // benchmark knob: 0 auto, 2 / 4 = queries per wave / 16
 
 static bool a16(const void* p, long ld) { return (((uintptr_t)p) & 15) == 0 && (ld % 8) == 0; }
 
 extern "C" {
+
+void pso_attention_set_variant(int v) {
+  g_attn_fwd_variant = v % 10;
+  g_attn_bwd_variant = v / 10;
+}
 
 int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
                       long sk_b, const void* v, long ldv, long sv_b, float scale, void* o, long ldo, long so_b,
@@ -534,14 +632,19 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.sq_b = sq_b; a.sk_b = sk_b; a.sv_b = sv_b;
   a.o = (bf16_t*)o; a.ldo = ldo; a.so_b = so_b; a.lse = lse;
   a.Sq = Sq; a.Sk = Sk; a.H = H; a.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(cdiv(Sq, 128), H, B);
-  attn_fwd_kernel<<<grid, ATT_THREADS, 0, (hipStream_t)stream>>>(a);
+  // 256 queries per workgroup (4 x 64-row waves) when that still gives >= 2 rounds of the 512 co-resident
+  // workgroups, else 128 (4 x 32): fewer K/V LDS bytes per MFMA vs. a fuller grid
+  const int nq4 = cdiv(Sq, 256), nq2 = cdiv(Sq, 128);
+  const bool big = g_attn_fwd_variant == 4 || (g_attn_fwd_variant == 0 && (long)nq4 * H * B >= 1024);
+  if (big) attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
+  else attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
   return pso_check_launch("pso_attention_fwd");
 }
 
 size_t pso_attention_bwd_ws_bytes(int B, int H, int Sq, int Sk) {
   size_t d = (size_t)B * H * Sq * sizeof(float);
-  size_t acc = (Sk <= 256) ? 2 * (size_t)B * Sk * H * ATT_D * sizeof(float) : 0;
+  const int qs = cross_qsplit(B, H, Sq, Sk);
+  size_t acc = qs > 1 ? 2 * (size_t)qs * B * Sk * H * ATT_D * sizeof(float) : 0;
   return ((d + 255) / 256) * 256 + acc;
 }
 
@@ -568,26 +671,39 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   a.lddq = lddq; a.lddk = lddk; a.lddv = lddv; a.sdq_b = sdq_b; a.sdk_b = sdk_b; a.sdv_b = sdv_b;
   const size_t doff = (((size_t)B * H * Sq * sizeof(float) + 255) / 256) * 256;
   const int nkb = cdiv(Sk, 128);
-  int qsplit = 1;
-  if (Sk <= 256) {  // few key blocks (cross-attention over 77 text tokens): split the query sweep, fp32 atomics
-    const int nqt = cdiv(Sq, ATT_KT);
-    qsplit = nqt < 16 ? nqt : 16;
+  const int qsplit = cross_qsplit(B, H, Sq, Sk);
+  const long part = (long)B * Sk * H * ATT_D;  // elements of one split slice
+  if (qsplit > 1) {
     a.dk_acc = (float*)((char*)ws + doff);
-    a.dv_acc = a.dk_acc + (size_t)B * Sk * H * ATT_D;
-    hipMemsetAsync(a.dk_acc, 0, 2 * (size_t)B * Sk * H * ATT_D * sizeof(float), st);
+    a.dv_acc = a.dk_acc + qsplit * part;
   }
   a.q_split = qsplit;
+  a.nbatch = B;
   attn_delta_kernel<<<cdiv((long)B * Sq, 4), 256, 0, st>>>(a, B);
-  attn_bwd_dkv_kernel<<<dim3(nkb * qsplit, H, B), ATT_THREADS, 0, st>>>(a);
+  // keys per wave: 32 (2 x 16, 128 keys per workgroup, 2 workgroups per CU); 64 on request (benchmark knob)
+  const int nkb4 = cdiv(Sk, 256);
+  const bool kj4 = g_attn_bwd_variant == 4;  // measured slower on every UNet shape (1 wave/SIMD, AGPR spills)
+  if (kj4) {
+    const size_t shm = 3 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    static bool attr4 = false;
+    if (!attr4) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<4, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm);
+      attr4 = true;
+    }
+    attn_bwd_dkv_kernel<4, 3><<<nkb4 * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb4);
+  } else {
+    const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    attn_bwd_dkv_kernel<2, 2><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
+  }
   attn_bwd_dq_kernel<<<dim3(cdiv(Sq, 128), H, B), ATT_THREADS, 0, st>>>(a);
   if (qsplit > 1) {
+    // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)
     const long rows = (long)B * Sk;
     const int cols = H * ATT_D;
-    // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)
-    f32_to_bf16_strided_kernel<<<cdiv(rows * cols, 256) > 4096 ? 4096 : cdiv(rows * cols, 256), 256, 0, st>>>(
-        rows, cols, a.dk_acc, (bf16_t*)dk, lddk);
-    f32_to_bf16_strided_kernel<<<cdiv(rows * cols, 256) > 4096 ? 4096 : cdiv(rows * cols, 256), 256, 0, st>>>(
-        rows, cols, a.dv_acc, (bf16_t*)dv, lddv);
+    const int nb = cdiv(rows * cols / 4, 256) > 2048 ? 2048 : cdiv(rows * cols / 4, 256);
+    reduce_splits_kernel<<<nb, 256, 0, st>>>(rows, cols, qsplit, a.dk_acc, part, (bf16_t*)dk, lddk);
+    reduce_splits_kernel<<<nb, 256, 0, st>>>(rows, cols, qsplit, a.dv_acc, part, (bf16_t*)dv, lddv);
   }
   return pso_check_launch("pso_attention_bwd");
 }

@@ -16,9 +16,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
   return __builtin_bit_cast(bf16_t, b);
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  // one v_cvt_pk_bf16_f32 (RNE, NaN-preserving) for both halves
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{lo, hi}), bf16x2_t));
 }
+// raw v_exp_f32 (2^x; results below 2^-126 flush to 0 -- fine for softmax weights, saves the denormal range fix-up)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll

@@ -83,6 +83,36 @@ def test_attention_fwd_bwd(cuda, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("variant", [2, 4])
+@pytest.mark.parametrize("B,H,Sq,Sk", [(2, 2, 256, 256), (2, 5, 300, 77), (1, 4, 130, 1000), (3, 20, 1024, 1024)])
+def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
+    """Both tile shapes of the forward (128 / 256 queries per workgroup) and of the dK/dV kernel (128 / 256 keys per
+    workgroup) on partial query and key tiles."""
+    from pairwise_sample_optimization_amd import kernels as K
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(Sq * 7 + Sk)
+    q = torch.randn(B, Sq, C, device=cuda, generator=g).bfloat16()
+    k = torch.randn(B, Sk, C, device=cuda, generator=g).bfloat16()
+    v = torch.randn(B, Sk, C, device=cuda, generator=g).bfloat16()
+    do = torch.randn(B, Sq, C, device=cuda, generator=g).bfloat16()
+    K.lib().pso_attention_set_variant(variant * 11)  # same tile choice for the forward and the dK/dV kernel
+    try:
+        o, lse = K.attention_fwd(q, k, v, H)
+        dq, dk, dv = K.attention_bwd(q, k, v, o, lse, do, H)
+    finally:
+        K.lib().pso_attention_set_variant(0)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, H)
+    assert _rel(o, ref) < 1e-2
+    f = lambda t: t.float().reshape(B, t.shape[1], H, 64).transpose(1, 2)
+    ref_lse = torch.logsumexp(f(q) @ f(k).transpose(-1, -2) * 0.125, dim=-1)
+    assert (lse - ref_lse).abs().max().item() < 2e-3
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    assert _rel(dq, gq) < 2e-2
+    assert _rel(dk, gk) < 2e-2
+    assert _rel(dv, gv) < 2e-2
+
+
 def test_geglu_silu_temb(cuda):
     from pairwise_sample_optimization_amd import kernels as K
     h = torch.randn(300, 2 * 640, device=cuda).bfloat16()

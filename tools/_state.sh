@@ -7,6 +7,8 @@ cat gpurun_out/bench.json; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench.err; exi
 timeout -k 10 300 python tools/shape_prof.py > gpurun_out/shape_prof.txt 2>&1; rc=$?
 head -40 gpurun_out/shape_prof.txt
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemm_bench.txt 2>&1; rc=$?
-cat gpurun_out/gemm_bench.txt
+if [ -n "$GEMM" ]; then
+  timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemm_bench.txt 2>&1; rc=$?
+  cat gpurun_out/gemm_bench.txt
+fi
 exit $rc
