@@ -113,6 +113,15 @@ void pso_attention_set_variant(int v);
  * dB = s dy^T u, reduction over tokens) without materialising transposes; split-K with f32 atomics. */
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream);
+/* Grouped (block-diagonal) form of pso_gemm_tn for the fused q/k/v LoRA adapters: with A = [M][I] the big side and
+ * B = [M][J] the rank side (J = r * I / group), out[i][j] += alpha * sum_m A[m][i] B[m][(i / group) * r + j % r]
+ * restricted to j in that group's r columns (out is [I][r]).  group = 0: plain pso_gemm_tn. */
+int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                        long ldo, int group, void* stream);
+/* Grouped (block-diagonal) skinny product for the fused q/k/v LoRA adapters of the backward (v = dy sB per adapter):
+ * out[m][g*N + n] = alpha * sum_k A[m][g*K + k] * W[n][g*K + k] for g < groups (bf16 out, N <= 128, N % 4 == 0). */
+int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
+                            void* out, long ldo, int groups, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).

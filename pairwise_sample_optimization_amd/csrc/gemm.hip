@@ -460,7 +460,9 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 
 int pso_gemm_skinny_nt(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha, void* out,
-                       long ldo, int out_f32, int accumulate, hipStream_t st);
+                       long ldo, int out_f32, int accumulate, int groups, hipStream_t st);
+int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long ldu, int R, int group_c, float alpha,
+                     float* out, long ldo, int out_jc, hipStream_t st);
 
 static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
@@ -481,7 +483,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g_gemm_variant == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
       (g.N % 4) == 0 && g.vec_ok && g.M >= 256)
     return pso_gemm_skinny_nt(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.alpha, g.out, g.ldo,
-                              g.out_dtype == PSO_F32, g.accumulate, st);
+                              g.out_dtype == PSO_F32, g.accumulate, 1, st);
   // Small outputs with a long reduction: split K over blocks, f32 atomics in the epilogue.
   const bool can_split = g.out_dtype == PSO_F32 && g.accumulate && !g.bias && !g.rowbias && !g.resid &&
                          !g.conv.mode && g.tail_group_n == 0;
@@ -712,14 +714,39 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
 }
 
 void pso_gemm_set_variant(int v) { g_gemm_variant = v; }
-void pso_gemm_tn_set_split(int ks) { g_tn_split = ks; }
+
+int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
+                            void* out, long ldo, int groups, void* stream) {
+  PSO_ARG_CHECK(M > 0 && N > 0 && N <= 128 && (N % 4) == 0 && K > 0 && (K % 8) == 0 && groups >= 1 && A && W && out,
+                "pso_gemm_skinny_grouped: need 0 < N <= 128, N %% 4 == 0, K %% 8 == 0");
+  PSO_ARG_CHECK(al16(A) && al16(W) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0,
+                "pso_gemm_skinny_grouped: alignment");
+  return pso_gemm_skinny_nt(M, N, K, A, lda, W, ldw, alpha, out, ldo, 0, 0, groups, (hipStream_t)stream);
+}
 
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream) {
+  return pso_gemm_tn_grouped(M, I, J, A, lda, B, ldb, alpha, out, ldo, 0, stream);
+}
+void pso_gemm_tn_set_split(int ks) { g_tn_split = ks; }
+
+int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                        long ldo, int group, void* stream) {
   PSO_ARG_CHECK(M >= 0 && I > 0 && J > 0 && A && B && out, "pso_gemm_tn: bad args");
   PSO_ARG_CHECK(al16(A) && al16(B) && (lda % 8) == 0 && (ldb % 8) == 0 && (I % 8) == 0 && (J % 8) == 0,
                 "pso_gemm_tn: operands need 16-B aligned rows and I, J multiples of 8");
   if (M == 0) return PSO_OK;
+  // One side a rank-r projection (LoRA): the streaming rank kernel.  group > 0 (block-diagonal fused q/k/v): the big
+  // side's column c pairs with the small side's columns [(c / group) * r, +r) where r = small width / (big / group).
+  auto rk = [](int r) { return r == 32 || r == 64 || r == 96; };
+  if (g_tn_split == 0) {
+    if (I % 128 == 0 && (group == 0 ? rk(J) : (group % 128 == 0 && I % group == 0 && rk(J / (I / group)))))
+      return pso_gemm_tn_rank(M, I, A, lda, B, ldb, group ? J / (I / group) : J, group, alpha, out, ldo, 0,
+                              (hipStream_t)stream);
+    if (J % 128 == 0 && group == 0 && rk(I))
+      return pso_gemm_tn_rank(M, J, B, ldb, A, lda, I, 0, alpha, out, ldo, 1, (hipStream_t)stream);
+  }
+  PSO_ARG_CHECK(group == 0, "pso_gemm_tn: grouped form needs a rank-32/64/96 side and 128 | group");
   const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
   const int nkt = (M + 63) / 64;
   // ~160 blocks: fewer leaves the M-range latency-bound, more multiplies the f32 atomics (measured optimum on the

@@ -1,0 +1,174 @@
+// Rank-r TN GEMM for gfx950: the LoRA weight gradients of the SDXL UNet.
+//
+//   D[c][j] = alpha * sum_m X[m][c] * U[m][j]      X: [M][C] (C >= 128, the activation / output gradient stream)
+//                                                  U: [M][R] (R = 16*NJT = 32 / 64 / 96, the rank-r projection)
+// accumulated (f32 atomics) into out[c][j] (dB = s dY^T u) or out[j][c] (dA = v^T x).  Replaces the reduction over the
+// B*S tokens inside peft's lora_A / lora_B weight gradients (`T:857` backward through `T:338-345`).
+//
+// The product is an HBM stream of X (2 FLOP per byte at R = 32).  Every 4-wave workgroup owns 128 columns of X and a
+// contiguous range of rows; 64-row steps of X (two 64 x 64 transposed-read images) and U (one or two images) go
+// global -> LDS directly (global_load_lds_dwordx4, source-side swizzle chunk ^ 2*((row >> 1) & 3)) through a 3-stage
+// ring with two steps in flight behind a counted vmcnt and one s_barrier per step.  Both MFMA operands are read
+// with ds_read_b64_tr_b16 (rows permuted identically inside each 32-deep step).  Rows past M load from a zero page.
+// `group_c` > 0: the U columns used by X column c start at (c / group_c) * R (the fused q/k/v adapters: dqkv columns
+// [jC, (j+1)C) pair with u_qkv columns [j r, (j+1) r)).
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void tnr_lds_void;
+typedef __attribute__((address_space(3))) s16x4 tnr_lds_s16x4;
+__device__ __attribute__((aligned(16))) uint4 g_tnr_zero[4];
+
+constexpr int TNR_IMG = 64 * 64;  // one 64-row x 64-column bf16 image
+
+__device__ __forceinline__ int tnr_swz(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 3) << 1)) << 3); }
+
+// lane i of each 16-lane group: column col0 + i of rows r0 .. r0+3 (r0 per group)
+__device__ __forceinline__ s16x4 tnr_tr(const bf16_t* img, int r0, int col0, int lane) {
+  const int li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = col0 + 4 * p;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((tnr_lds_s16x4*)(img + tnr_swz(r0 + q, col >> 3) + (col & 7)));
+}
+__device__ __forceinline__ bf16x8 tnr_frag(const bf16_t* img, int m0, int col0, int lane) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const int g = lane >> 4;
+  const s16x4 a = tnr_tr(img, m0 + 4 * g, col0, lane), b = tnr_tr(img, m0 + 16 + 4 * g, col0, lane);
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NJT, bool OUT_JC>
+__global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int M, int C, const bf16_t* __restrict__ X, long ldx,
+                                                              const bf16_t* __restrict__ U, long ldu, int group_c,
+                                                              float alpha, float* __restrict__ out, long ldo,
+                                                              int steps_per_block) {
+  constexpr int R = 16 * NJT;
+  constexpr int UIMG = (R + 63) / 64;
+  constexpr int STG = 3;
+  constexpr int STAGE = (2 + UIMG) * TNR_IMG;
+  constexpr int PIECES = 2 * 2 + (UIMG * 8 + 3) / 4;  // X: 16 pieces / 4 waves; U: 8 per image
+  __shared__ __attribute__((aligned(16))) bf16_t lds[STG * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, cl = lane & 15;
+  const int ncb = C / 128;
+  const int cb = blockIdx.x % ncb, mb = blockIdx.x / ncb;
+  const int c0 = cb * 128;
+  const int u_off = group_c > 0 ? (c0 / group_c) * R : 0;
+  const int nsteps_all = (M + 63) / 64;
+  const int s_beg = mb * steps_per_block;
+  const int s_end = min(nsteps_all, s_beg + steps_per_block);
+  const int n = s_end > s_beg ? s_end - s_beg : 0;
+
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lc = pch ^ (2 * ((prow >> 1) & 3));  // logical source chunk of this lane's physical chunk
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_tnr_zero);
+  auto issue = [&](int st, int buf) {
+    bf16_t* base = lds + buf * STAGE;
+    // X: pieces 0..15 = (image xi = piece / 8, rows (piece % 8) * 8 ..); wave w issues pieces 4w .. 4w+3
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave * 4 + i;
+      const int xi = piece >> 3, pr = piece & 7;
+      const int m = st * 64 + pr * 8 + prow;
+      const bf16_t* src = m < M ? X + (long)m * ldx + c0 + xi * 64 + lc * 8 : zero;
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src), (tnr_lds_void*)(base + xi * TNR_IMG + pr * 8 * 64),
+                                       16, 0, 0);
+    }
+    // U: UIMG images x 8 pieces, dealt round-robin over the waves
+#pragma unroll
+    for (int i = 0; i < (UIMG * 8 + 3) / 4; ++i) {
+      const int piece = wave + 4 * i;
+      if (piece < UIMG * 8) {
+        const int ui = piece >> 3, pr = piece & 7;
+        const int m = st * 64 + pr * 8 + prow;
+        const int col = ui * 64 + lc * 8;
+        const bf16_t* src = (m < M && col < R) ? U + (long)m * ldu + u_off + col : zero;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(src),
+                                         (tnr_lds_void*)(base + (2 + ui) * TNR_IMG + pr * 8 * 64), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[2][NJT];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int j = 0; j < NJT; ++j) acc[ci][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (n > 0) issue(s_beg, 0);
+  if (n > 1) issue(s_beg + 1, 1);
+  for (int i = 0; i < n; ++i) {
+    // every wave issues the same number of pieces per step (padding pieces included), so vmcnt counts match
+    if (i + 1 < n) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (i + 2 < n) issue(s_beg + i + 2, (i + 2) % STG);
+    const bf16_t* base = lds + (i % STG) * STAGE;
+    // wave w owns X columns c0 + 32w .. +32 = image (w >> 1), columns (w & 1) * 32 ..
+    const bf16_t* ximg = base + (wave >> 1) * TNR_IMG;
+    const int xcol = (wave & 1) * 32;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 xf[2], uf[NJT];
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) xf[ci] = tnr_frag(ximg, ks * 32, xcol + ci * 16, lane);
+#pragma unroll
+      for (int j = 0; j < NJT; ++j) uf[j] = tnr_frag(base + (2 + (j >> 2)) * TNR_IMG, ks * 32, (j & 3) * 16, lane);
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int j = 0; j < NJT; ++j) {
+          if (OUT_JC)  // lane holds D^T[j = 16j' + 4g + r][c = 16ci + cl]: consecutive lanes -> consecutive c
+            acc[ci][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(uf[j], xf[ci], acc[ci][j], 0, 0, 0);
+          else  // lane holds D[c = 16ci + 4g + r][j = 16j' + cl]
+            acc[ci][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ci], uf[j], acc[ci][j], 0, 0, 0);
+        }
+    }
+  }
+  if (n == 0) return;
+  const int cw = c0 + wave * 32;
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int j = 0; j < NJT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (OUT_JC) atomicAdd(out + (long)(j * 16 + 4 * g + r) * ldo + cw + ci * 16 + cl, acc[ci][j][r] * alpha);
+        else atomicAdd(out + (long)(cw + ci * 16 + 4 * g + r) * ldo + j * 16 + cl, acc[ci][j][r] * alpha);
+      }
+}
+
+template <int NJT>
+int launch_tnr(int M, int C, const bf16_t* X, long ldx, const bf16_t* U, long ldu, int group_c, float alpha, float* out,
+               long ldo, bool out_jc, hipStream_t st) {
+  const int ncb = C / 128;
+  const int nsteps = (M + 63) / 64;
+  // ~2 workgroups per CU, at least 3 steps each (two in flight behind the one being multiplied)
+  int nmb = (512 + ncb - 1) / ncb;
+  int spb = (nsteps + nmb - 1) / nmb;
+  if (spb < 3) spb = 3;
+  nmb = (nsteps + spb - 1) / spb;
+  const dim3 grid(ncb * nmb);
+  if (out_jc)
+    gemm_tn_rank_kernel<NJT, true><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
+  else
+    gemm_tn_rank_kernel<NJT, false><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
+  return pso_check_launch("pso_gemm_tn(rank)");
+}
+
+}  // namespace
+
+// host entry used by pso_gemm_tn (gemm.hip) when one side is a rank-r projection: C % 128 == 0, R in {32, 64, 96},
+// 16-B aligned rows (checked there).
+int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long ldu, int R, int group_c, float alpha,
+                     float* out, long ldo, int out_jc, hipStream_t st) {
+  auto x = (const bf16_t*)X;
+  auto u = (const bf16_t*)U;
+  switch (R) {
+    case 32: return launch_tnr<2>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
+    case 64: return launch_tnr<4>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
+    case 96: return launch_tnr<6>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
+    default: pso_set_error("pso_gemm_tn(rank): R must be 32, 64 or 96"); return PSO_ERR_ARG;
+  }
+}

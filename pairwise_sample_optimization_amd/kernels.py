@@ -66,15 +66,36 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
     return out
 
 
-def gemm_tn(a, b, out, alpha=1.0):
-    """out[I,J] (f32, accumulated) += alpha * a^T @ b  with a [M,I], b [M,J] (row-strided views)."""
+def gemm_grouped_skinny(a, w, groups, out=None, alpha=1.0):
+    """Block-diagonal skinny product: out[:, g*N:(g+1)*N] = alpha * a[:, g*K:(g+1)*K] @ w[:, g*K:(g+1)*K]^T, bf16."""
+    M, KG = a.shape
+    N = w.shape[0]
+    Kg = KG // groups
+    assert w.shape[1] == KG and KG == Kg * groups
+    if out is None:
+        out = torch.empty((M, groups * N), device=a.device, dtype=BF16)
+    e0 = _prof_begin()
+    check(lib().pso_gemm_skinny_grouped(M, N, Kg, ptr(a), _row_stride(a), ptr(w), _row_stride(w), float(alpha),
+                                        ptr(out), _row_stride(out), int(groups), stream_ptr()), "pso_gemm_skinny_grouped")
+    _prof_end(e0, 2.0 * M * N * KG, 2.0 * (M * KG + N * KG + M * N * groups), ("gemm_grouped", M, N, KG, groups))
+    return out
+
+
+TN_RANKS = (32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
+
+
+def gemm_tn(a, b, out, alpha=1.0, group=0):
+    """out[I,J] (f32, accumulated) += alpha * a^T @ b  with a [M,I], b [M,J] (row-strided views).
+    group > 0 (block-diagonal, fused q/k/v adapters): out [I, r] with r = J * group / I; column block
+    a[:, g*group:(g+1)*group] pairs with b[:, g*r:(g+1)*r]."""
     M, I = a.shape
     J = b.shape[1]
-    assert b.shape[0] == M and out.shape == (I, J) and out.dtype == torch.float32
+    r = J * group // I if group else J
+    assert b.shape[0] == M and out.shape == (I, r) and out.dtype == torch.float32
     e0 = _prof_begin()
-    check(lib().pso_gemm_tn(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
-                            _row_stride(out), stream_ptr()), "pso_gemm_tn")
-    _prof_end(e0, 2.0 * M * I * J, 2.0 * M * (I + J) + 8.0 * I * J, ("gemm_tn", M, I, J))
+    check(lib().pso_gemm_tn_grouped(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
+                                    _row_stride(out), int(group), stream_ptr()), "pso_gemm_tn")
+    _prof_end(e0, 2.0 * M * I * r, 2.0 * M * (I + J) + 8.0 * I * r, ("gemm_tn", M, I, J, group))
     return out
 
 

@@ -421,14 +421,15 @@ class BasicTransformerBlock(nn.Module):
             K.gemm_tn(v_q2, sv["n2"], g("attn2.A_q"))
             K.gemm_tn(dq2, sv["u_q2"], g("attn2.B_q"), st.scale)
             # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
-            v_kv = torch.empty((B * Se, 2 * r), device=dh3.device, dtype=BF16)
-            K.gemm(dkv2[:, :C], L.sBt_kv2[:, :C], out=v_kv[:, :r])
-            K.gemm(dkv2[:, C:], L.sBt_kv2[:, C:], out=v_kv[:, r:])
+            v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
             K.gemm_tn(v_kv, rt.enc, g("attn2.A_kv"))
             gB = g("attn2.B_kv")
             u_kv2 = sv["u_kv2"]
-            K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
-            K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
+            if r in K.TN_RANKS:
+                K.gemm_tn(dkv2, u_kv2, gB, st.scale, group=C)
+            else:
+                K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
+                K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
@@ -447,15 +448,17 @@ class BasicTransformerBlock(nn.Module):
         K.attention_bwd(q3[..., :C], q3[..., C:2 * C], q3[..., 2 * C:], sv["a1"].view(B, S, C), sv["lse1"],
                         da1.view(B, S, C), a1m.heads, dq=d3[..., :C], dk=d3[..., C:2 * C], dv=d3[..., 2 * C:])
         if lo:
-            v_qkv = torch.empty((M, 3 * r), device=dh3.device, dtype=BF16)
-            for j in range(3):
-                K.gemm(dqkv[:, j * C:(j + 1) * C], L.sBt_qkv[:, j * C:(j + 1) * C], out=v_qkv[:, j * r:(j + 1) * r])
+            v_qkv = K.gemm_grouped_skinny(dqkv, L.sBt_qkv, 3)
             dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv)
             K.gemm_tn(v_qkv, sv["n1"], g("attn1.A_qkv"))
             gB = g("attn1.B_qkv")
             u_qkv = sv["u_qkv"]
-            for j in range(3):
-                K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C], st.scale)
+            if r in K.TN_RANKS:
+                K.gemm_tn(dqkv, u_qkv, gB, st.scale, group=C)
+            else:
+                for j in range(3):
+                    K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
+                              st.scale)
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv)
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)

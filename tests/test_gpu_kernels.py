@@ -108,8 +108,11 @@ def test_conv_stride1_input_grad_flipped(cuda):
     assert _rel(_nchw(out), gx) < 1e-5
 
 
-@pytest.mark.parametrize("M,I,J", [(16384, 96, 640), (308, 32, 2048), (4096, 1280, 32), (100, 64, 8)])
+@pytest.mark.parametrize("M,I,J", [(16384, 96, 640), (308, 32, 2048), (4096, 1280, 32), (100, 64, 8),
+                                   (8192, 1280, 32), (8192, 32, 1280), (8192, 96, 1280), (616, 64, 2048),
+                                   (1000, 640, 64), (616, 1280, 32), (77, 32, 256)])
 def test_gemm_tn_vs_fp32(cuda, M, I, J):
+    """Generic TN path and the streaming rank-r path (one side 32 / 64 / 96 wide), partial 64-row steps included."""
     from pairwise_sample_optimization_amd import kernels as K_
     big = torch.randn(M, I + 16, device=cuda).bfloat16()
     a = big[:, 8:8 + I]          # column-slice view (row stride != I)
@@ -117,6 +120,32 @@ def test_gemm_tn_vs_fp32(cuda, M, I, J):
     out = torch.randn(I, J, device=cuda)
     ref = out + 0.5 * (a.float().t() @ b.float())
     K_.gemm_tn(a, b, out, alpha=0.5)
+    assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,C,G", [(8192, 1280, 3), (1000, 640, 3), (616, 1280, 2)])
+def test_gemm_grouped_skinny(cuda, M, C, G):
+    """Block-diagonal v = dy sB of the fused q/k/v (G = 3) and cross k/v (G = 2) adapters."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    a = torch.randn(M, G * C, device=cuda).bfloat16()
+    w = (torch.randn(32, G * C, device=cuda) / 30).bfloat16()
+    out = K_.gemm_grouped_skinny(a, w, G)
+    ref = torch.cat([a[:, j * C:(j + 1) * C].float() @ w[:, j * C:(j + 1) * C].float().t() for j in range(G)], 1)
+    assert out.shape == (M, 32 * G)
+    assert _rel(out, ref) < 8e-3
+
+
+@pytest.mark.parametrize("M,C", [(8192, 1280), (1000, 640)])
+def test_gemm_tn_grouped(cuda, M, C):
+    """Block-diagonal q/k/v form: out[jC + i][:] += dqkv[:, jC + i]^T u_qkv[:, j*32:(j+1)*32]."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    a = torch.randn(M, 3 * C, device=cuda).bfloat16()
+    u = torch.randn(M, 96, device=cuda).bfloat16()
+    out = torch.randn(3 * C, 32, device=cuda)
+    ref = out.clone()
+    for j in range(3):
+        ref[j * C:(j + 1) * C] += 0.25 * (a[:, j * C:(j + 1) * C].float().t() @ u[:, 32 * j:32 * (j + 1)].float())
+    K_.gemm_tn(a, u, out, alpha=0.25, group=C)
     assert _rel(out, ref) < 1e-5
 
 
@@ -177,7 +206,8 @@ def test_conv_every_variant_large(cuda, variant):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 32, 1280), (4096, 96, 1280), (16384, 32, 640), (300, 100, 136),
-                                   (1000, 64, 2048), (257, 128, 72), (4096, 4, 40)])
+                                   (1000, 64, 2048), (257, 128, 72), (4096, 4, 40), (32768, 32, 640),
+                                   (8192, 96, 1280), (616, 64, 2048), (20000, 48, 320)])
 def test_gemm_skinny_n(cuda, M, N, K):
     """LoRA-rank products (N <= 128): bf16 out, strided A view, f32 accumulate; ragged M / K tails."""
     from pairwise_sample_optimization_amd import kernels as K_

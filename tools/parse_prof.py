@@ -11,11 +11,11 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILY = ("gemm_bf16_kernel", "gemm_tn_kernel")
+FAMILY = ("gemm_bf16_kernel", "gemm_tn", "gemm_skinny")
 
 
 def short(name):
-    n = name.replace("void ", "")
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
     return n.split("(")[0][:90]
 
 

@@ -5,11 +5,11 @@ import csv
 import sys
 from collections import defaultdict
 
-FAMILY = ("gemm_bf16_kernel", "gemm_tn_kernel", "gemm_skinny")
+FAMILY = ("gemm_bf16_kernel", "gemm_tn", "gemm_skinny")
 
 
 def short(name):
-    n = name.replace("void ", "")
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
     return n.split("(")[0][:80]
 
 
