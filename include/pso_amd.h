@@ -123,6 +123,17 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
 int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
                             void* out, long ldo, int groups, void* stream);
 
+/* GEGLU feed-forward projection with the activation fused into the GEMM epilogue (diffusers GEGLU, `net.0`):
+ * w is the proj weight [N][K] with its rows INTERLEAVED per 64 as [h rows 32 | gate rows 32] (bias likewise), N =
+ * 2F, N % 256 == 0.  out [M][F] = h * gelu(gate) (exact erf GELU, h / gate rounded to bf16 first, as the unfused
+ * path does); out_pre (optional) [M][N] receives the interleaved pre-activation the backward needs. */
+int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* bias, void* out,
+                   long ldo, void* out_pre, long ld_pre, void* stream);
+/* Backward of the GEGLU fused into the GEMM producing its output gradient: dout = a . w^T ([M][N], N = F, rounded to
+ * bf16), pre = the interleaved pre-activation [M][2F]; out [M][2F] = interleaved [dout*gelu(g) | dout*h*gelu'(g)]. */
+int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* pre,
+                       long ld_pre, void* out, long ldo, void* stream);
+
 /* ------------------------------------------------------------------------------------------------------------------
  * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).
  * Input = channel concat of src1 [B][H][W][C1] and src2 [B][H][W][C2] (C2 may be 0); output [B][Ho][Wo][Cout] (ldo).

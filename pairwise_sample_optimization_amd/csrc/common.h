@@ -25,6 +25,15 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 // raw v_exp_f32 (2^x; results below 2^-126 flush to 0 -- fine for softmax weights, saves the denormal range fix-up)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// exact (erf) GELU and its derivative: diffusers GEGLU -> F.gelu(approximate="none")
+__device__ __forceinline__ float gelu_erf(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float g) {
+  const float cdf = 0.5f * (1.f + erff(g * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * g * g);
+  return cdf + g * pdf;
+}
+__device__ __forceinline__ float bf_round(float x) { return bf2f(f2bf(x)); }
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

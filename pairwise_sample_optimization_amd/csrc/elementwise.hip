@@ -30,12 +30,6 @@ static int grid_for(long n, int per_thread = 1) {
 
 #define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
 
-__device__ __forceinline__ float gelu_erf(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float g) {
-  const float cdf = 0.5f * (1.f + erff(g * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * g * g);
-  return cdf + g * pdf;
-}
 
 // in [M][ld_in] holding [h | gate] (F each); out [M][F] = h * gelu(gate)
 __global__ void geglu_fwd_kernel(long M, int F, const bf16_t* __restrict__ in, long ldi, bf16_t* __restrict__ out,

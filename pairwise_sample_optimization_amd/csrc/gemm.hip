@@ -45,7 +45,18 @@ struct GemmArgs {
   const bf16_t* resid; long ldr;
   void* out; long ldo; int out_dtype; int accumulate;
   int vec_ok;  // 4-wide epilogue vectors are aligned
+  int group_m;  // tile rows per raster group (>= 1)
+  // GEGLU epilogues (diffusers GEGLU: [h | gate] = x W^T + b, out = h * gelu(gate)), weight rows interleaved per 64
+  // columns as [h 32 | gate 32]:  EPI_GEGLU writes out = h*gelu(gate) (N/2 columns) and, if out2, the interleaved
+  // pre-activation;  EPI_GEGLU_BWD takes the GEMM result as dout (N columns), aux = interleaved pre-activation, and
+  // writes the interleaved input gradient [dout*gelu(g) | dout*h*gelu'(g)] to out (2N columns).
+  void* out2; long ldo2;
+  const bf16_t* aux; long ldaux;
 };
+
+#define EPI_NONE 0
+#define EPI_GEGLU 1
+#define EPI_GEGLU_BWD 2
 
 __device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ (r & 7)) << 3); }
 
@@ -130,7 +141,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 // row R holds logical chunk p ^ (R & 7) -- the same involution swz() applies on the read side.
 // WM x WN waves, each owning a (BM/WM) x (BN/WN) accumulator tile; STAGES-deep LDS ring with STAGES-1 K-tiles of
 // direct-to-LDS loads in flight behind a counted vmcnt and a raw s_barrier (a __syncthreads() would drain them).
-template <int BM, int BN, int CONV, int WM, int WN, int STAGES, bool PIPE = false>
+template <int BM, int BN, int CONV, int WM, int WN, int STAGES, bool PIPE = false, int EPI = EPI_NONE>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int WAVES = WM * WN;
   using T = Tile<BM, BN, WAVES>;
@@ -154,7 +165,18 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     const int q = nblk / 8, r = nblk % 8, x = bid % 8;
     if (nblk >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
-  const int bm = bid / nbn, bn = bid - (bid / nbn) * nbn;
+  // grouped raster: runs of g.group_m tile rows are walked column by column, so the tiles an XCD's CUs hold at once
+  // share A row-panels and B column-panels in its L2 (group_m = 1: plain row-major)
+  int bm, bn;
+  {
+    const int gm = g.group_m;
+    const int per_group = gm * nbn;
+    const int grp = bid / per_group, first_m = grp * gm;
+    const int gsz = min(nbm - first_m, gm);
+    const int in = bid - grp * per_group;
+    bm = first_m + in % gsz;
+    bn = in / gsz;
+  }
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int nt1 = (g.K1 + BK - 1) / BK;
@@ -369,6 +391,68 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   }  // !PIPE
 
   // ---- epilogue: lane holds out[m][n0..n0+3] for each (i, j) ----
+  if constexpr (EPI == EPI_GEGLU) {
+    // this wave's 64 columns = one interleaved group: subtiles j = 0,1 hold h, j = 2,3 the matching gate columns.
+    // h and gate are rounded to bf16 first (the unfused path stores them in bf16 before the GEGLU).
+    static_assert(NJ == 4, "GEGLU epilogue needs 64-column wave tiles");
+    const int ng = n0 + wn * 64;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int nh = ng + jj * 16 + fk * 4;
+        float vh[4], vg[4], o[4];
+        const uint2 bh = *reinterpret_cast<const uint2*>(g.bias + nh);
+        const uint2 bg = *reinterpret_cast<const uint2*>(g.bias + nh + 32);
+        const float bhv[4] = {bf2f(bh.x & 0xffff), bf2f(bh.x >> 16), bf2f(bh.y & 0xffff), bf2f(bh.y >> 16)};
+        const float bgv[4] = {bf2f(bg.x & 0xffff), bf2f(bg.x >> 16), bf2f(bg.y & 0xffff), bf2f(bg.y >> 16)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vh[r] = bf_round(acc[i][jj][r] * g.alpha + bhv[r]);
+          vg[r] = bf_round(acc[i][jj + 2][r] * g.alpha + bgv[r]);
+          o[r] = vh[r] * gelu_erf(vg[r]);
+        }
+        if (g.out2) {
+          bf16_t* p = reinterpret_cast<bf16_t*>(g.out2) + (long)m * g.ldo2 + nh;
+          *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(vh[0], vh[1]), pack2bf(vh[2], vh[3]));
+          *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(vg[0], vg[1]), pack2bf(vg[2], vg[3]));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ng / 2 + jj * 16 + fk * 4) =
+            make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      }
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_GEGLU_BWD) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
+        if (n >= g.N) continue;
+        const int ph = (n >> 5) * 64 + (n & 31);  // interleaved position of h (gate at +32)
+        const uint2 hv = *reinterpret_cast<const uint2*>(g.aux + (long)m * g.ldaux + ph);
+        const uint2 gv = *reinterpret_cast<const uint2*>(g.aux + (long)m * g.ldaux + ph + 32);
+        const float h[4] = {bf2f(hv.x & 0xffff), bf2f(hv.x >> 16), bf2f(hv.y & 0xffff), bf2f(hv.y >> 16)};
+        const float gt[4] = {bf2f(gv.x & 0xffff), bf2f(gv.x >> 16), bf2f(gv.y & 0xffff), bf2f(gv.y >> 16)};
+        float dh[4], dg[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = bf_round(acc[i][j][r] * g.alpha);  // the unfused path stores dout in bf16
+          dh[r] = d * gelu_erf(gt[r]);
+          dg[r] = d * h[r] * gelu_erf_grad(gt[r]);
+        }
+        bf16_t* p = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
+        *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(dh[0], dh[1]), pack2bf(dh[2], dh[3]));
+        *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(dg[0], dg[1]), pack2bf(dg[2], dg[3]));
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * (BM / WM) + i * 16 + fr;
@@ -427,31 +511,40 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   }
 }
 
-template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2, bool PIPE = false>
+template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2, bool PIPE = false, int EPI = EPI_NONE>
 static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   dim3 grid(nblk, ksplit);
   const int threads = 64 * WM * WN;
   const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
   static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
+  if constexpr (EPI != EPI_NONE) {  // fused-activation epilogues: dense operands only
+    if (!attr_done) {
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE, EPI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      attr_done = true;
+    }
+    gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE, EPI><<<grid, threads, shm, st>>>(g);
+    return pso_check_launch("pso_gemm(geglu)");
+  }
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
   switch (g.conv.mode) {
     case PSO_CONV_NORMAL:
-      gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g);
+      gemm_bf16_kernel<BM, BN, PSO_CONV_NORMAL, WM, WN, STAGES, PIPE, EPI><<<grid, threads, shm, st>>>(g);
       break;
-    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g); break;
-    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g); break;
-    default: gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE><<<grid, threads, shm, st>>>(g);
+    case PSO_CONV_UP2: gemm_bf16_kernel<BM, BN, PSO_CONV_UP2, WM, WN, STAGES, PIPE, EPI><<<grid, threads, shm, st>>>(g); break;
+    case PSO_CONV_T2: gemm_bf16_kernel<BM, BN, PSO_CONV_T2, WM, WN, STAGES, PIPE, EPI><<<grid, threads, shm, st>>>(g); break;
+    default: gemm_bf16_kernel<BM, BN, 0, WM, WN, STAGES, PIPE, EPI><<<grid, threads, shm, st>>>(g);
   }
   return pso_check_launch("pso_gemm");
 }
@@ -467,8 +560,11 @@ int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long 
 static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
+static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
+
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
     pso_set_error("pso_gemm: tail_group_n must be a multiple of 64");
     return PSO_ERR_ARG;
@@ -713,7 +809,52 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   return run_gemm(g, (hipStream_t)stream);
 }
 
-void pso_gemm_set_variant(int v) { g_gemm_variant = v; }
+int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* bias, void* out,
+                   long ldo, void* out_pre, long ld_pre, void* stream) {
+  PSO_ARG_CHECK(M > 0 && N > 0 && (N % 256) == 0 && K > 0 && (K % 8) == 0 && a && w && bias && out,
+                "pso_gemm_geglu: need N %% 256 == 0, K %% 8 == 0, bias");
+  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0 && al8(bias) &&
+                    (!out_pre || (al8(out_pre) && (ld_pre % 4) == 0)),
+                "pso_gemm_geglu: alignment");
+  PSO_ARG_CHECK((long)M * lda < 0x7fffffffL && (long)N * ldw < 0x7fffffffL, "pso_gemm_geglu: operand too large");
+  GemmArgs g{};
+  g.a1 = (const bf16_t*)a; g.lda1 = lda; g.K1 = K;
+  g.b1 = (const bf16_t*)w; g.ldb1 = ldw;
+  g.M = M; g.N = N; g.alpha = 1.f;
+  g.bias = (const bf16_t*)bias;
+  g.out = out; g.ldo = ldo; g.out_dtype = PSO_BF16;
+  g.out2 = out_pre; g.ldo2 = ld_pre;
+  g.vec_ok = 1; g.rows_per_group = 1;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  return launch<256, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
+}
+
+int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* pre,
+                       long ld_pre, void* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(M > 0 && N > 0 && (N % 32) == 0 && K > 0 && (K % 8) == 0 && a && w && pre && out,
+                "pso_gemm_geglu_bwd: need N %% 32 == 0, K %% 8 == 0");
+  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0 && al8(pre) &&
+                    (ld_pre % 4) == 0,
+                "pso_gemm_geglu_bwd: alignment");
+  PSO_ARG_CHECK((long)M * lda < 0x7fffffffL && (long)N * ldw < 0x7fffffffL, "pso_gemm_geglu_bwd: operand too large");
+  GemmArgs g{};
+  g.a1 = (const bf16_t*)a; g.lda1 = lda; g.K1 = K;
+  g.b1 = (const bf16_t*)w; g.ldb1 = ldw;
+  g.M = M; g.N = N; g.alpha = 1.f;
+  g.out = out; g.ldo = ldo; g.out_dtype = PSO_BF16;
+  g.aux = (const bf16_t*)pre; g.ldaux = ld_pre;
+  g.vec_ok = 1; g.rows_per_group = 1;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  const hipStream_t st = (hipStream_t)stream;
+  const long t160 = (long)((M + 127) / 128) * ((N + 159) / 160);
+  if ((N % 160) == 0 && t160 >= 256) return launch<128, 160, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);
+  return launch<64, 64, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);
+}
+
+void pso_gemm_set_variant(int v) {
+  g_gemm_variant = v % 100;
+  g_gemm_group = v / 100;
+}
 
 int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
                             void* out, long ldo, int groups, void* stream) {

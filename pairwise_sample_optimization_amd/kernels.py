@@ -81,6 +81,44 @@ def gemm_grouped_skinny(a, w, groups, out=None, alpha=1.0):
     return out
 
 
+def geglu_interleave_index(F, device=None):
+    """Row order of the GEGLU proj weight for the fused epilogue: per 32 outputs, [h rows 32 | gate rows 32]."""
+    g = torch.arange(F // 32, device=device).view(-1, 1)
+    j = torch.arange(32, device=device).view(1, -1)
+    return torch.cat([g * 32 + j, F + g * 32 + j], 1).reshape(-1)
+
+
+def gemm_geglu(a, w_int, b_int, out_pre=None, out=None):
+    """diffusers GEGLU with the activation in the GEMM epilogue: out [M, F] = h * gelu(gate) where
+    [h | gate] = a @ W^T + b, given the interleaved weight / bias (geglu_interleave_index).  out_pre (optional)
+    [M, 2F] receives the interleaved pre-activation for the backward."""
+    M, Kd = a.shape
+    N = w_int.shape[0]
+    if out is None:
+        out = torch.empty((M, N // 2), device=a.device, dtype=BF16)
+    e0 = _prof_begin()
+    check(lib().pso_gemm_geglu(M, N, ptr(a), _row_stride(a), Kd, ptr(w_int), _row_stride(w_int), ptr(b_int),
+                               ptr(out), _row_stride(out), ptr(out_pre),
+                               _row_stride(out_pre) if out_pre is not None else 0, stream_ptr()), "pso_gemm_geglu")
+    _prof_end(e0, 2.0 * M * N * Kd, 2.0 * (M * Kd + N * Kd + M * N // 2 + (M * N if out_pre is not None else 0)),
+              ("gemm_geglu", M, N, Kd, out_pre is not None))
+    return out
+
+
+def gemm_geglu_bwd(a, w, pre, out=None):
+    """Input gradient of the fused GEGLU: dout = a @ w^T ([M, F], F = w rows), pre = interleaved pre-activation
+    [M, 2F]; returns the interleaved [dout*gelu(g) | dout*h*gelu'(g)] [M, 2F]."""
+    M, Kd = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, 2 * N), device=a.device, dtype=BF16)
+    e0 = _prof_begin()
+    check(lib().pso_gemm_geglu_bwd(M, N, ptr(a), _row_stride(a), Kd, ptr(w), _row_stride(w), ptr(pre),
+                                   _row_stride(pre), ptr(out), _row_stride(out), stream_ptr()), "pso_gemm_geglu_bwd")
+    _prof_end(e0, 2.0 * M * N * Kd, 2.0 * (M * Kd + N * Kd + 4 * M * N), ("gemm_geglu_bwd", M, N, Kd))
+    return out
+
+
 TN_RANKS = (32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
 
 

@@ -371,9 +371,10 @@ class BasicTransformerBlock(nn.Module):
             h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
         # --- GEGLU feed-forward ---
         n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
-        f = K.gemm(n3, self.ff.proj.weight, bias=self.ff.proj.bias)
-        gg = K.geglu_fwd(f)
-        h3 = K.gemm(gg, self.ff.out.weight, bias=self.ff.out.bias, resid=h2)
+        ff = self.ff
+        f = torch.empty((M, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
+        gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f)  # f: interleaved pre-activation (backward only)
+        h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
         if rt.save:
             sv = dict(x=x, st1=st1, n1=n1, qkv=qkv, a1=a1, lse1=lse1, h1=h1, st2=st2, n2=n2, q2=q2, kv2=kv2, a2=a2,
                       lse2=lse2, h2=h2, st3=st3, f=f)
@@ -382,7 +383,7 @@ class BasicTransformerBlock(nn.Module):
             rt.saved.append(sv)
         return h3
 
-    def bwd(self, dh3, sv, rt, path):
+    def bwd(self, dh3, sv, rt, path, need_dx=True):
         C = self.dim
         B = rt.B
         M = dh3.shape[0]
@@ -394,9 +395,8 @@ class BasicTransformerBlock(nn.Module):
         g = (lambda k: st.grad_seg(path, k)) if lo else None
         a1m, a2m = self.attn1, self.attn2
         # --- FF ---
-        dg = K.gemm(dh3, self.ff.out.wt)
-        df = K.geglu_bwd(sv["f"], dg)
-        dn3 = K.gemm(df, self.ff.proj.wt)
+        df = K.gemm_geglu_bwd(dh3, self.ff.out.wt, sv["f"])  # interleaved d[h | gate]
+        dn3 = K.gemm(df, self.ff.wt_int)
         dh2 = K.layer_norm_bwd(sv["h2"], dn3, sv["st3"], self.norm3.weight, dadd=dh3)
         # --- cross attention out-proj:  y = a W^T + (a A^T)(sB)^T ;  v = dy sB ; da = dy W + v A ---
         o2 = a2m.to_out[0]
@@ -449,7 +449,7 @@ class BasicTransformerBlock(nn.Module):
                         da1.view(B, S, C), a1m.heads, dq=d3[..., :C], dk=d3[..., C:2 * C], dv=d3[..., 2 * C:])
         if lo:
             v_qkv = K.gemm_grouped_skinny(dqkv, L.sBt_qkv, 3)
-            dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv)
+            dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv) if need_dx else None
             K.gemm_tn(v_qkv, sv["n1"], g("attn1.A_qkv"))
             gB = g("attn1.B_qkv")
             u_qkv = sv["u_qkv"]
@@ -460,7 +460,9 @@ class BasicTransformerBlock(nn.Module):
                     K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
                               st.scale)
         else:
-            dn1 = K.gemm(dqkv, a1m.wt_qkv)
+            dn1 = K.gemm(dqkv, a1m.wt_qkv) if need_dx else None
+        if not need_dx:  # first adapter block: nothing below it needs a gradient
+            return None
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
 
 
@@ -473,7 +475,13 @@ class SimpleFF(nn.Module):
         self.out = Linear(4 * dim, dim)
 
     def prepare(self):
-        self.proj.prepare()
+        # rows interleaved per 32 outputs as [h 32 | gate 32] so the GEMM epilogue holds both halves of a GEGLU
+        # output in one lane (pso_gemm_geglu); the pre-activation and its gradient live in that order internally
+        F = self.out.in_features
+        idx = K.geglu_interleave_index(F, self.proj.weight.device)
+        self.w_int = self.proj.weight.data[idx].contiguous()
+        self.b_int = self.proj.bias.data[idx].contiguous()
+        self.wt_int = K.transpose(self.w_int)  # [dim][2F] for the input gradient
         self.out.prepare()
 
     def _remap(self):
@@ -508,13 +516,16 @@ class Transformer2DModel(nn.Module):
             h = blk.fwd(h, rt, f"{path}.transformer_blocks.{i}")
         return K.gemm(h, self.proj_out.weight, bias=self.proj_out.bias, resid=x.view(-1, C)).view(B, H, W, C)
 
-    def bwd(self, dy, rt, path):
+    def bwd(self, dy, rt, path, need_dx=True):
         B, H, W, C = dy.shape
         d2 = dy.view(-1, C)
         dh = K.gemm(d2, self.proj_out.wt)
         for i in reversed(range(len(self.transformer_blocks))):
-            dh = self.transformer_blocks[i].bwd(dh, rt.saved.pop(), rt, f"{path}.transformer_blocks.{i}")
+            dh = self.transformer_blocks[i].bwd(dh, rt.saved.pop(), rt, f"{path}.transformer_blocks.{i}",
+                                                need_dx=need_dx or i > 0)
         sv = rt.saved.pop()
+        if not need_dx:
+            return None
         dn = K.gemm(dh, self.proj_in.wt).view(B, H, W, C)
         return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy)
 
@@ -861,20 +872,34 @@ class UNet2DConditionModel(nn.Module):
         dh = m.resnets[1].bwd(dh, rt)
         dh = m.attentions[0].bwd(dh, rt, "mid_block.attentions.0")
         dh = m.resnets[0].bwd(dh, rt)
-        # the up-block backward visits skips in forward-push order, so the down-block backward takes them from the end
-        for i in reversed(range(len(self.down_blocks))):
+        # the up-block backward visits skips in forward-push order, so the down-block backward takes them from the end.
+        # Below the first adapter-carrying attention (down_blocks.1.attentions.0) nothing has a trainable parameter and
+        # the latent needs no gradient, so the backward stops there: down_blocks.0 (two 128^2 resnets + downsample),
+        # down_blocks.1.resnets.0 and conv_in are never differentiated (the reference's autograd also runs them only
+        # for the input gradient, which is then discarded).
+        i0, j0 = self._first_attn
+        for i in reversed(range(i0, len(self.down_blocks))):
             blk = self.down_blocks[i]
             if hasattr(blk, "downsamplers"):
                 dh = K.add(dh, skip_grads.pop())
                 dh = blk.downsamplers[0].bwd(dh, rt)
             for j in reversed(range(len(blk.resnets))):
                 dh = K.add(dh, skip_grads.pop())
+                if (i, j) == (i0, j0):
+                    blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}", need_dx=False)
+                    break
                 if hasattr(blk, "attentions"):
                     dh = blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}")
                 dh = blk.resnets[j].bwd(dh, rt)
-        # remaining skip (conv_in output) -- conv_in has no trainable params and x needs no grad
-        assert len(skip_grads) == 1 and not rt.saved, (len(skip_grads), len(rt.saved))
+        rt.saved.clear()  # activations of the never-differentiated prefix
         return None
+
+    @property
+    def _first_attn(self):
+        for i, blk in enumerate(self.down_blocks):
+            if hasattr(blk, "attentions"):
+                return i, 0
+        raise ValueError("UNet without attention blocks has no adapter to train")
 
     # ---------------- diffusers call surface ----------------
     def forward(self, sample, timestep, encoder_hidden_states, added_cond_kwargs=None, return_dict=True, **kw):

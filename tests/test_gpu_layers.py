@@ -3,6 +3,7 @@ import math
 
 import pytest
 import torch
+
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
@@ -111,6 +112,32 @@ def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
     assert _rel(dq, gq) < 2e-2
     assert _rel(dk, gk) < 2e-2
     assert _rel(dv, gv) < 2e-2
+
+
+@pytest.mark.parametrize("M,dim", [(8192, 1280), (300, 64), (1000, 640)])
+def test_gemm_geglu_fused(cuda, M, dim):
+    """GEGLU in the GEMM epilogue (interleaved weight rows) and its backward fused into the dout GEMM, vs torch fp32."""
+    from pairwise_sample_optimization_amd import kernels as K
+    Fd = 4 * dim
+    g = torch.Generator(device="cuda").manual_seed(M + dim)
+    x = torch.randn(M, dim, device=cuda, generator=g).bfloat16()
+    w = (torch.randn(2 * Fd, dim, device=cuda, generator=g) / dim ** 0.5).bfloat16()
+    b = (0.1 * torch.randn(2 * Fd, device=cuda, generator=g)).bfloat16()
+    idx = K.geglu_interleave_index(Fd, cuda)
+    pre = torch.empty(M, 2 * Fd, device=cuda, dtype=torch.bfloat16)
+    out = K.gemm_geglu(x, w[idx].contiguous(), b[idx].contiguous(), out_pre=pre)
+    fr = (x.float() @ w.float().t() + b.float()).requires_grad_(True)
+    h, gt = fr.chunk(2, dim=-1)
+    ref = h * F.gelu(gt)
+    assert _rel(out, ref) < 8e-3
+    assert _rel(pre, fr[:, idx]) < 4e-3
+    # backward: dout = dy @ Wout (dy [M, dim], Wout^T rows = [F][dim])
+    dy = torch.randn(M, dim, device=cuda, generator=g).bfloat16()
+    wout_t = (torch.randn(Fd, dim, device=cuda, generator=g) / dim ** 0.5).bfloat16()
+    dpre = K.gemm_geglu_bwd(dy, wout_t, pre)
+    dout = dy.float() @ wout_t.float().t()
+    (gref,) = torch.autograd.grad(ref, fr, dout)
+    assert _rel(dpre, gref[:, idx]) < 1.5e-2
 
 
 def test_geglu_silu_temb(cuda):
