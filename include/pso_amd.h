@@ -93,11 +93,13 @@ int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_pre
  * All A/B operands are bf16 with K contiguous; K1, K2 multiples of 8; rows 16-B aligned.
  * tail_group_n > 0 (multiple of 64): output columns [j*tail_group_n, (j+1)*tail_group_n) take their K2-tail from A2
  * columns [j*K2, (j+1)*K2) -- three LoRA adapters (q, k, v) fused into one QKV projection with B2 = [3C][r].
+ * tail_rows > 0: only rows m < tail_rows take the K2-tail (A2 then has tail_rows rows) -- the policy (LoRA on) and
+ * reference (adapters disabled, T:790-805) images of one micro-step ride in one pass, policy rows first.
  * ---------------------------------------------------------------------------------------------------------------- */
 int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
-             int tail_group_n, void* stream);
+             int tail_group_n, int tail_rows, void* stream);
 
 /* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
  * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
@@ -126,9 +128,10 @@ int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const 
 /* GEGLU feed-forward projection with the activation fused into the GEMM epilogue (diffusers GEGLU, `net.0`):
  * w is the proj weight [N][K] with its rows INTERLEAVED per 64 as [h rows 32 | gate rows 32] (bias likewise), N =
  * 2F, N % 256 == 0.  out [M][F] = h * gelu(gate) (exact erf GELU, h / gate rounded to bf16 first, as the unfused
- * path does); out_pre (optional) [M][N] receives the interleaved pre-activation the backward needs. */
+ * path does); out_pre (optional) receives the interleaved pre-activation the backward needs, rows < pre_rows only
+ * (pre_rows = 0: all M rows). */
 int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* bias, void* out,
-                   long ldo, void* out_pre, long ld_pre, void* stream);
+                   long ldo, void* out_pre, long ld_pre, int pre_rows, void* stream);
 /* Backward of the GEGLU fused into the GEMM producing its output gradient: dout = a . w^T ([M][N], N = F, rounded to
  * bf16), pre = the interleaved pre-activation [M][2F]; out [M][2F] = interleaved [dout*gelu(g) | dout*h*gelu'(g)]. */
 int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* pre,

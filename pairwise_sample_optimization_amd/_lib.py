@@ -37,14 +37,14 @@ SIGNATURES = {
     "pso_pair_loss_fwd": (ci, [ci, ci, ci, vp, vp, vp, vp, ci, vp, vp, cf, cf, vp, vp, vp, csz, vp]),
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
-                      ci, vp]),
+                      ci, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
     "pso_gemm_tn_set_split": (None, [ci]),
     "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_gemm_tn_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
     "pso_gemm_skinny_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
-    "pso_gemm_geglu": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, vp, cl, vp, cl, vp]),
+    "pso_gemm_geglu": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, vp, cl, vp, cl, ci, vp]),
     "pso_gemm_geglu_bwd": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),

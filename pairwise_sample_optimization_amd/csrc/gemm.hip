@@ -37,6 +37,7 @@ struct GemmArgs {
   const bf16_t* a2; long lda2; int K2;
   const bf16_t* b2; long ldb2;
   int tail_group_n;  // >0: the A2 tail of output columns [j*G, (j+1)*G) starts at A2 column j*K2
+  int tail_m;        // rows >= tail_m get no A2 tail (policy + reference images in one pass: LoRA on the first rows)
   int M, N;
   ConvGeom conv;
   float alpha;
@@ -278,10 +279,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       for (int i = 0; i < T::A_CH; ++i) {
         const int piece = wave * T::A_CH + i;
         const int R = piece * 8 + prow;
-        const int m = min(m0 + R, g.M - 1);
+        const int mr = m0 + R;
+        const int m = min(mr, g.tail_m - 1);
         const int k = k0 + lcA[i] * 8;
         const bf16_t* src = g.a2 + a2_off + (long)m * g.lda2 + k;
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(k < g.K2 ? src : zero), (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>((k < g.K2 && mr < g.tail_m) ? src : zero),
+                                         (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           vg[r] = bf_round(acc[i][jj + 2][r] * g.alpha + bgv[r]);
           o[r] = vh[r] * gelu_erf(vg[r]);
         }
-        if (g.out2) {
+        if (g.out2 && m < g.tail_m) {  // pre-activation rows kept for the backward (policy rows of a paired pass)
           bf16_t* p = reinterpret_cast<bf16_t*>(g.out2) + (long)m * g.ldo2 + nh;
           *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(vh[0], vh[1]), pack2bf(vh[2], vh[3]));
           *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(vg[0], vg[1]), pack2bf(vg[2], vg[3]));
@@ -753,7 +756,7 @@ extern "C" {
 int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
-             int tail_group_n, void* stream) {
+             int tail_group_n, int tail_rows, void* stream) {
   PSO_ARG_CHECK(M >= 0 && N >= 0 && K1 >= 0 && (K1 % 8) == 0, "pso_gemm: need K1 %% 8 == 0 (K1=%d)", K1);
   PSO_ARG_CHECK(a1 && b1 && out, "pso_gemm: null operand");
   PSO_ARG_CHECK(al16(a1) && al16(b1) && (lda1 % 8) == 0 && (ldb1 % 8) == 0, "pso_gemm: A1/B1 must be 16-B aligned rows");
@@ -770,6 +773,7 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
   g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
   g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
   g.tail_group_n = a2 ? tail_group_n : 0;
+  g.tail_m = (tail_rows > 0 && tail_rows < M) ? tail_rows : M;
   g.M = M; g.N = N;
   g.alpha = alpha;
   g.bias = (const bf16_t*)bias;
@@ -799,6 +803,7 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
   g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
   g.M = B * Ho * Wo; g.N = Cout;
+  g.tail_m = g.M;
   g.conv.mode = mode; g.conv.src2 = (const bf16_t*)src2; g.conv.C1 = C1; g.conv.C2 = C2;
   g.conv.H = H; g.conv.W = W; g.conv.Ho = Ho; g.conv.Wo = Wo; g.conv.ks = ks; g.conv.stride = stride; g.conv.pad = pad;
   g.alpha = alpha;
@@ -810,7 +815,7 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
 }
 
 int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* bias, void* out,
-                   long ldo, void* out_pre, long ld_pre, void* stream) {
+                   long ldo, void* out_pre, long ld_pre, int pre_rows, void* stream) {
   PSO_ARG_CHECK(M > 0 && N > 0 && (N % 256) == 0 && K > 0 && (K % 8) == 0 && a && w && bias && out,
                 "pso_gemm_geglu: need N %% 256 == 0, K %% 8 == 0, bias");
   PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0 && al8(bias) &&
@@ -824,6 +829,7 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   g.bias = (const bf16_t*)bias;
   g.out = out; g.ldo = ldo; g.out_dtype = PSO_BF16;
   g.out2 = out_pre; g.ldo2 = ld_pre;
+  g.tail_m = (pre_rows > 0 && pre_rows < M) ? pre_rows : M;
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
   return launch<256, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);

@@ -38,9 +38,10 @@ def _row_stride(t):
 
 
 def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=None, rows_per_group=1, out=None,
-         out_dtype=BF16, accumulate=False, tail_group_n=0):
+         out_dtype=BF16, accumulate=False, tail_group_n=0, tail_rows=0):
     """out[M,N] = alpha*(a @ w^T + a2 @ w2^T) + bias + rowbias[m // rows_per_group] + resid.
-    tail_group_n > 0: output column group j uses a2[:, j*K2:(j+1)*K2] with w2 [N, K2]."""
+    tail_group_n > 0: output column group j uses a2[:, j*K2:(j+1)*K2] with w2 [N, K2].
+    tail_rows > 0: only the first tail_rows rows take the a2 term (a2 has tail_rows rows)."""
     require_cuda(a, w)
     M, K1 = a.shape
     N = w.shape[0]
@@ -48,7 +49,7 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
     K2 = 0
     if a2 is not None:
         K2 = w2.shape[1]
-        assert w2.shape[0] == N and a2.shape[0] == M
+        assert w2.shape[0] == N and a2.shape[0] == (tail_rows if tail_rows else M)
         assert a2.shape[1] == (K2 * (N // tail_group_n) if tail_group_n else K2)
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=out_dtype)
@@ -59,7 +60,7 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
                          float(alpha), ptr(bias), ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
                          int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
                          ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
-                         stream_ptr()), "pso_gemm")
+                         int(tail_rows), stream_ptr()), "pso_gemm")
     _prof_end(e0, 2.0 * M * N * (K1 + K2),
               2.0 * (M * (K1 + (a2.shape[1] if a2 is not None else 0)) + N * (K1 + K2)) + out.element_size() * M * N,
               ("gemm", M, N, K1, K2, tail_group_n, out.dtype == torch.float32))
@@ -88,10 +89,10 @@ def geglu_interleave_index(F, device=None):
     return torch.cat([g * 32 + j, F + g * 32 + j], 1).reshape(-1)
 
 
-def gemm_geglu(a, w_int, b_int, out_pre=None, out=None):
+def gemm_geglu(a, w_int, b_int, out_pre=None, out=None, pre_rows=0):
     """diffusers GEGLU with the activation in the GEMM epilogue: out [M, F] = h * gelu(gate) where
     [h | gate] = a @ W^T + b, given the interleaved weight / bias (geglu_interleave_index).  out_pre (optional)
-    [M, 2F] receives the interleaved pre-activation for the backward."""
+    [pre_rows or M, 2F] receives the interleaved pre-activation of the first pre_rows rows for the backward."""
     M, Kd = a.shape
     N = w_int.shape[0]
     if out is None:
@@ -99,7 +100,8 @@ def gemm_geglu(a, w_int, b_int, out_pre=None, out=None):
     e0 = _prof_begin()
     check(lib().pso_gemm_geglu(M, N, ptr(a), _row_stride(a), Kd, ptr(w_int), _row_stride(w_int), ptr(b_int),
                                ptr(out), _row_stride(out), ptr(out_pre),
-                               _row_stride(out_pre) if out_pre is not None else 0, stream_ptr()), "pso_gemm_geglu")
+                               _row_stride(out_pre) if out_pre is not None else 0, int(pre_rows), stream_ptr()),
+          "pso_gemm_geglu")
     _prof_end(e0, 2.0 * M * N * Kd, 2.0 * (M * Kd + N * Kd + M * N // 2 + (M * N if out_pre is not None else 0)),
               ("gemm_geglu", M, N, Kd, out_pre is not None))
     return out

@@ -254,11 +254,10 @@ class PSOTrainer:
         P = self.P * count
         u = self.unet
         u.enable_adapters()
-        eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
-        u.disable_adapters()
-        with torch.no_grad():
-            eps_ref, _ = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
-        u.enable_adapters()
+        # policy (LoRA on, T:775-787) and reference (adapters disabled, T:790-805) eps of the same inputs in ONE pass
+        eps_both, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True, paired_ref=True)
+        n = mb.unet_in.shape[0]
+        eps_pol, eps_ref = eps_both[:n], eps_both[n:]
         idx = None
         if self.mode == MODE_TURBO and self.m > 1:  # sample_compare draws a reward column per pair (T:405)
             idx = torch.randint(0, self.m, (P,), device=mb.x.device, generator=generator)

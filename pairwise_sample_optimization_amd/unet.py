@@ -332,11 +332,15 @@ class BasicTransformerBlock(nn.Module):
         lo = rt.lora_on
         L = rt.lora.blk[path] if lo else None
         r = rt.r
+        # paired pass (policy images first, then their reference copies): the adapters act on the first Mp rows only
+        Mp = M // 2 if rt.paired else M
+        tr = Mp if rt.paired else 0
+        pol = (lambda t: t[:t.shape[0] // 2]) if rt.paired else (lambda t: t)
         # --- self attention: fused q/k/v projection, the three LoRA up-projections as a grouped K-tail ---
         n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
         if lo:
-            u_qkv = K.gemm(n1, L.A_qkv)                                     # [M, 3r]
-            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C)
+            u_qkv = K.gemm(pol(n1), L.A_qkv)                                # [Mp, 3r]
+            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
         else:
             qkv = K.gemm(n1, a1m.w_qkv)
         q3 = qkv.view(B, S, 3 * C)
@@ -344,8 +348,8 @@ class BasicTransformerBlock(nn.Module):
         a1 = a1.view(M, C)
         o1 = a1m.to_out[0]
         if lo:
-            u_o1 = K.gemm(a1, L.A_o1)
-            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1)
+            u_o1 = K.gemm(pol(a1), L.A_o1)
+            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1, tail_rows=tr)
         else:
             h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x)
         # --- cross attention over the 77 text tokens ---
@@ -353,10 +357,11 @@ class BasicTransformerBlock(nn.Module):
         enc = rt.enc  # [B*77, Dc]
         Se = enc.shape[0] // B
         if lo:
-            u_q2 = K.gemm(n2, L.A_q2)
-            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2)
-            u_kv2 = K.gemm(enc, L.A_kv2)                                    # [B*77, 2r]
-            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=L.sB_kv2, tail_group_n=C)
+            u_q2 = K.gemm(pol(n2), L.A_q2)
+            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
+            u_kv2 = K.gemm(pol(enc), L.A_kv2)                               # [Bp*77, 2r]
+            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=L.sB_kv2, tail_group_n=C,
+                         tail_rows=enc.shape[0] // 2 if rt.paired else 0)
         else:
             q2 = K.gemm(n2, a2m.to_q.weight)
             kv2 = K.gemm(enc, a2m.w_kv)
@@ -365,19 +370,20 @@ class BasicTransformerBlock(nn.Module):
         a2 = a2.view(M, C)
         o2 = a2m.to_out[0]
         if lo:
-            u_o2 = K.gemm(a2, L.A_o2)
-            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2)
+            u_o2 = K.gemm(pol(a2), L.A_o2)
+            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2, tail_rows=tr)
         else:
             h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
         # --- GEGLU feed-forward ---
         n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
         ff = self.ff
-        f = torch.empty((M, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
-        gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f)  # f: interleaved pre-activation (backward only)
+        f = torch.empty((Mp, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
+        gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f, pre_rows=Mp)  # f: interleaved pre-activation (bwd)
         h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
-        if rt.save:
-            sv = dict(x=x, st1=st1, n1=n1, qkv=qkv, a1=a1, lse1=lse1, h1=h1, st2=st2, n2=n2, q2=q2, kv2=kv2, a2=a2,
-                      lse2=lse2, h2=h2, st3=st3, f=f)
+        if rt.save:  # the backward runs on the policy images only
+            sv = dict(x=pol(x), st1=pol(st1), n1=pol(n1), qkv=pol(qkv), a1=pol(a1), lse1=pol(lse1), h1=pol(h1),
+                      st2=pol(st2), n2=pol(n2), q2=pol(q2), kv2=pol(kv2), a2=pol(a2), lse2=pol(lse2), h2=pol(h2),
+                      st3=pol(st3), f=f)
             if lo:
                 sv.update(u_qkv=u_qkv, u_o1=u_o1, u_q2=u_q2, u_kv2=u_kv2, u_o2=u_o2)
             rt.saved.append(sv)
@@ -511,7 +517,7 @@ class Transformer2DModel(nn.Module):
         xn, st = K.group_norm_fwd(x, self.norm.weight, self.norm.bias, self.groups, 1e-6, False)
         h = K.gemm(xn.view(-1, C), self.proj_in.weight, bias=self.proj_in.bias)
         if rt.save:
-            rt.saved.append({"x": x, "st": st})
+            rt.saved.append({"x": rt.pol(x), "st": rt.pol(st)})
         for i, blk in enumerate(self.transformer_blocks):
             h = blk.fwd(h, rt, f"{path}.transformer_blocks.{i}")
         return K.gemm(h, self.proj_out.weight, bias=self.proj_out.bias, resid=x.view(-1, C)).view(B, H, W, C)
@@ -560,7 +566,7 @@ class ResnetBlock2D(nn.Module):
             sc = x
         out = K.conv2d(h2, self.conv2.w_nhwc, bias=self.conv2.bias, resid=sc)
         if rt.save:
-            rt.saved.append({"x": x, "st1": st1, "c1": c1, "st2": st2})
+            rt.saved.append({"x": rt.pol(x), "st1": rt.pol(st1), "c1": rt.pol(c1), "st2": rt.pol(st2)})
         return out
 
     def bwd(self, dout, rt):
@@ -781,7 +787,8 @@ class UNet2DConditionModel(nn.Module):
 
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
-        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on)
+        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False)
+        rt.pol = lambda t: t[:t.shape[0] // 2] if rt.paired else t
         rt.lora = self.lora
         rt.r = self.lora.r if lora_on else 0
         return rt
@@ -800,8 +807,14 @@ class UNet2DConditionModel(nn.Module):
         emb = K.gemm(K.silu(K.gemm(add_in, a1.weight, bias=a1.bias)), a2.weight, bias=a2.bias, resid=emb)
         return K.gemm(K.silu(emb), self._temb_w, bias=self._temb_b)  # [B, sum Co]
 
-    def forward_nhwc(self, x, timestep, enc, text_embeds, time_ids, save=False):
-        """Core forward.  x NHWC bf16 [B,h,w,4]; enc [B,77,Dc]; returns eps NHWC bf16 [B,h,w,4]."""
+    def forward_nhwc(self, x, timestep, enc, text_embeds, time_ids, save=False, paired_ref=False):
+        """Core forward.  x NHWC bf16 [B,h,w,4]; enc [B,77,Dc]; returns eps NHWC bf16 [B,h,w,4].
+
+        paired_ref=True (the PSO micro-step, T:775-805): ONE pass yields the policy eps (adapters on) AND the reference
+        eps (adapters disabled) of the same inputs, returned as [2B,h,w,4] = [policy; reference].  Everything below
+        the first adapter-carrying attention is adapter-free, so it runs once on the B images and is then duplicated;
+        from there on the batch is [policy; reference] and every adapter acts on the policy rows only (pso_gemm
+        tail_rows).  save=True keeps the policy half of what the backward needs."""
         if not self._prepared:
             self.prepare()
         B = x.shape[0]
@@ -815,8 +828,20 @@ class UNet2DConditionModel(nn.Module):
         cols = K.im2col3(x, self.conv_in.kp)
         h = K.gemm(cols, self.conv_in.w_col, bias=self.conv_in.bias).view(B, H, W, -1)
         skips = [h]
+        i0, j0 = self._first_attn
+        rt.save = False  # the prefix below the first adapter block is never differentiated (backward_nhwc)
         for i, blk in enumerate(self.down_blocks):
             for j, res in enumerate(blk.resnets):
+                if (i, j) == (i0, j0):  # entering the adapter-carrying part
+                    rt.save = save
+                    if paired_ref:
+                        dup = lambda t: torch.cat([t, t], 0)
+                        h = dup(h)
+                        skips = [dup(s_) for s_ in skips]
+                        temb_all = dup(temb_all)
+                        rt.enc = dup(rt.enc)
+                        rt.B = 2 * B
+                        rt.paired = True
                 h = res.fwd(h, rt, tb(res))
                 if hasattr(blk, "attentions"):
                     h = blk.attentions[j].fwd(h, rt, f"down_blocks.{i}.attentions.{j}")
@@ -832,7 +857,7 @@ class UNet2DConditionModel(nn.Module):
             for j, res in enumerate(blk.resnets):
                 s = skips.pop()
                 hc = K.concat_channels(h, s)
-                if save:
+                if rt.save:
                     rt.saved.append({"c1": h.shape[-1]})
                 h = res.fwd(hc, rt, tb(res))
                 if hasattr(blk, "attentions"):
@@ -843,7 +868,11 @@ class UNet2DConditionModel(nn.Module):
                                   self.cfg.norm_eps, True)
         out = K.conv2d(hn, self.conv_out.w_nhwc, bias=self.conv_out.bias)
         if save:
-            rt.saved.append({"h": h, "st": st})
+            rt.saved.append({"h": rt.pol(h), "st": rt.pol(st)})
+        # the backward sees the policy half only
+        rt.B = B
+        rt.enc = rt.pol(rt.enc)
+        rt.paired = False
         return out, rt
 
     def backward_nhwc(self, dout, rt):

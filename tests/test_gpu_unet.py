@@ -115,3 +115,34 @@ def test_unet_backward_bf16_torch_reference_noise(cuda):
     print(f"\n total rel err vs fp32: hip={tot(mine):.3e} torch-bf16={tot({k: v.grad for k, v in leaf16.items()}):.3e}")
     for a, b, k in rows:
         print(f"   hip={a:.3e} torch-bf16={b:.3e}  {k}")
+
+
+@pytest.mark.parametrize("which", ["tiny16", "sdxl32"])
+def test_paired_pass_equals_separate_passes(cuda, which):
+    """forward_nhwc(paired_ref=True): one pass = [policy eps (adapters on); reference eps (adapters off)] (T:775-805),
+    and its backward = the backward of a policy-only pass (the reference half carries no gradient)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    from pairwise_sample_optimization_amd.unet import UNetConfig
+    cfg = UNetConfig.tiny(16) if which == "tiny16" else UNetConfig.sdxl(32)
+    unet, sample, t, enc, text, tid = _setup(cuda, cfg)
+    x = K.nchw_to_nhwc(sample)
+    B = x.shape[0]
+    st = unet.lora
+    both, rt = unet.forward_nhwc(x, t, enc, text, tid, save=True, paired_ref=True)
+    dout = torch.randn_like(both[:B].float()).bfloat16()
+    st.grad.zero_()
+    unet.backward_nhwc(dout, rt)
+    g_pair = st.grad.clone()
+    pol, rt1 = unet.forward_nhwc(x, t, enc, text, tid, save=True)
+    st.grad.zero_()
+    unet.backward_nhwc(dout, rt1)
+    g_sep = st.grad.clone()
+    unet.disable_adapters()
+    with torch.no_grad():
+        ref, _ = unet.forward_nhwc(x, t, enc, text, tid)
+    unet.enable_adapters()
+    e_pol, e_ref, e_g = _rel(both[:B], pol), _rel(both[B:], ref), _rel(g_pair, g_sep)
+    print(f"{which}: paired vs separate: policy {e_pol:.2e} reference {e_ref:.2e} lora grads {e_g:.2e}")
+    assert both.shape[0] == 2 * B
+    assert e_pol < 1e-2 and e_ref < 1e-2 and e_g < 3e-2
+    assert (both[B:] - both[:B]).abs().max().item() > 0  # the adapters act on the policy half only
