@@ -429,29 +429,49 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     return;
   }
   if constexpr (EPI == EPI_GEGLU_BWD) {
+    // GEGLU backward epilogue, staged through LDS so every global access is a coalesced 16-B chunk: dout is rounded to
+    // bf16 into LDS (exactly what the unfused path stores), then the workgroup walks it in 8-column chunks, reading
+    // the interleaved pre-activation and writing the interleaved input gradient.
+    constexpr int TP = (BM * (BN + 8) * 2 <= STAGES * (BM + BN) * BK * 2) ? BN + 8 : BN;  // tile pitch (elements)
+    constexpr int NT = 64 * WM * WN;
+    __syncthreads();  // every wave is done with the operand ring
+    bf16_t* tl = lds_base;
+    const float bscale = g.alpha;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const int m = m0 + wm * (BM / WM) + i * 16 + fr;
-      if (m >= g.M) continue;
+      const int ml = wm * (BM / WM) + i * 16 + fr;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
-        if (n >= g.N) continue;
-        const int ph = (n >> 5) * 64 + (n & 31);  // interleaved position of h (gate at +32)
-        const uint2 hv = *reinterpret_cast<const uint2*>(g.aux + (long)m * g.ldaux + ph);
-        const uint2 gv = *reinterpret_cast<const uint2*>(g.aux + (long)m * g.ldaux + ph + 32);
-        const float h[4] = {bf2f(hv.x & 0xffff), bf2f(hv.x >> 16), bf2f(hv.y & 0xffff), bf2f(hv.y >> 16)};
-        const float gt[4] = {bf2f(gv.x & 0xffff), bf2f(gv.x >> 16), bf2f(gv.y & 0xffff), bf2f(gv.y >> 16)};
-        float dh[4], dg[4];
+        const int nl = wn * (BN / WN) + j * 16 + fk * 4;
+        float v[4] = {acc[i][j][0] * bscale, acc[i][j][1] * bscale, acc[i][j][2] * bscale, acc[i][j][3] * bscale};
+        *reinterpret_cast<uint2*>(tl + ml * TP + nl) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+    __syncthreads();
+    {
+      // dout chunk (row ml, columns c .. c+7 of the F-wide gradient) -> interleaved positions ph .. ph+7 (gate +32)
+      constexpr int CC = BN / 8;
+      for (int q = threadIdx.x; q < BM * CC; q += NT) {
+        const int ml = q / CC, cl = (q - (q / CC) * CC) * 8;
+        const int m = m0 + ml, n = n0 + cl;
+        if (m >= g.M || n >= g.N) continue;
+        const int ph = (n >> 5) * 64 + (n & 31);
+        const uint4 dv = *reinterpret_cast<const uint4*>(tl + ml * TP + cl);
+        const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph);
+        const uint4 gv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph + 32);
+        const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
+        uint32_t oh[4], og[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = bf_round(acc[i][j][r] * g.alpha);  // the unfused path stores dout in bf16
-          dh[r] = d * gelu_erf(gt[r]);
-          dg[r] = d * h[r] * gelu_erf_grad(gt[r]);
+        for (int e = 0; e < 4; ++e) {
+          const float d0 = bf2f(dw[e] & 0xffff), d1 = bf2f(dw[e] >> 16);
+          const float h0 = bf2f(hw[e] & 0xffff), h1 = bf2f(hw[e] >> 16);
+          const float g0 = bf2f(gw[e] & 0xffff), g1 = bf2f(gw[e] >> 16);
+          oh[e] = pack2bf(d0 * gelu_erf(g0), d1 * gelu_erf(g1));
+          og[e] = pack2bf(d0 * h0 * gelu_erf_grad(g0), d1 * h1 * gelu_erf_grad(g1));
         }
         bf16_t* p = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
-        *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(dh[0], dh[1]), pack2bf(dh[2], dh[3]));
-        *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(dg[0], dg[1]), pack2bf(dg[2], dg[3]));
+        *reinterpret_cast<uint4*>(p) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
+        *reinterpret_cast<uint4*>(p + 32) = make_uint4(og[0], og[1], og[2], og[3]);
       }
     }
     return;
@@ -818,9 +838,9 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
                    long ldo, void* out_pre, long ld_pre, int pre_rows, void* stream) {
   PSO_ARG_CHECK(M > 0 && N > 0 && (N % 256) == 0 && K > 0 && (K % 8) == 0 && a && w && bias && out,
                 "pso_gemm_geglu: need N %% 256 == 0, K %% 8 == 0, bias");
-  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0 && al8(bias) &&
-                    (!out_pre || (al8(out_pre) && (ld_pre % 4) == 0)),
-                "pso_gemm_geglu: alignment");
+  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al16(out) && (ldo % 8) == 0 && al8(bias) &&
+                    (!out_pre || (al16(out_pre) && (ld_pre % 8) == 0)),
+                "pso_gemm_geglu: alignment (16-B rows)");
   PSO_ARG_CHECK((long)M * lda < 0x7fffffffL && (long)N * ldw < 0x7fffffffL, "pso_gemm_geglu: operand too large");
   GemmArgs g{};
   g.a1 = (const bf16_t*)a; g.lda1 = lda; g.K1 = K;
@@ -839,9 +859,9 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
                        long ld_pre, void* out, long ldo, void* stream) {
   PSO_ARG_CHECK(M > 0 && N > 0 && (N % 32) == 0 && K > 0 && (K % 8) == 0 && a && w && pre && out,
                 "pso_gemm_geglu_bwd: need N %% 32 == 0, K %% 8 == 0");
-  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al8(out) && (ldo % 4) == 0 && al8(pre) &&
-                    (ld_pre % 4) == 0,
-                "pso_gemm_geglu_bwd: alignment");
+  PSO_ARG_CHECK(al16(a) && al16(w) && (lda % 8) == 0 && (ldw % 8) == 0 && al16(out) && (ldo % 8) == 0 && al16(pre) &&
+                    (ld_pre % 8) == 0,
+                "pso_gemm_geglu_bwd: alignment (16-B rows)");
   PSO_ARG_CHECK((long)M * lda < 0x7fffffffL && (long)N * ldw < 0x7fffffffL, "pso_gemm_geglu_bwd: operand too large");
   GemmArgs g{};
   g.a1 = (const bf16_t*)a; g.lda1 = lda; g.K1 = K;
