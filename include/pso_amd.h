@@ -45,6 +45,10 @@ extern "C" {
  *           log(sqrt(1-abar_prev)), log(sqrt(2*pi)), 0]                                                        */
 #define PSO_COEF_STRIDE 8
 
+/* DreamBooth PSO loss types (DB:1924-1929) */
+#define PSO_DB_SIGMOID 0 /* "pso":    -log sigmoid(beta * (ref_diff - model_diff)), reference eps required */
+#define PSO_DB_HINGE 1   /* "pso_db": relu(1 - beta * (-model_diff)) (the personalization/scripts recipe)    */
+
 const char* pso_last_error(void);
 int pso_abi_version(void);
 
@@ -136,6 +140,25 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
  * bf16), pre = the interleaved pre-activation [M][2F]; out [M][2F] = interleaved [dout*gelu(g) | dout*h*gelu'(g)]. */
 int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void* w, long ldw, const void* pre,
                        long ld_pre, void* out, long ldo, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * DreamBooth PSO loss (config 5), forward and backward to the UNet eps.
+ * Replaces: DB = personalization/train_pso_sdxl_turbo_dreambooth.py:1847-1935 -- EDM-style x0 = eps*(-sigma) + noisy,
+ *           per-image sigma^-2-weighted MSE vs the clean latent, instance/negative split, pso / pso_db loss, prior
+ *           loss -- and the autograd backward of it down to the UNet output (DB:1953).
+ * Layout: 2B images, instance b at row b, its negative at row B + b.  eps [2B][n] (eps_dtype), eps_ref the same
+ * (adapters disabled, loss_type PSO_DB_SIGMOID only), noisy / x0 fp32 [2B][n], sigma fp32 [2B].
+ * fwd outputs: losses_out [2B] (+ [2B] reference) per-image MSE, logits_out [B], loss_out [1]; ws (keep it for the
+ * bwd) holds the fp64 partials.  bwd: deps [2B][n] = (*grad_out or 1) * grad_scale * dL/d eps.
+ * ---------------------------------------------------------------------------------------------------------------- */
+size_t pso_db_loss_ws_bytes(int B, int n);
+int pso_db_loss_fwd(int loss_type, int B, int n, const void* eps, const void* eps_ref, int eps_dtype,
+                    const float* noisy, const float* x0, const float* sigma, float beta, float neg_defactor,
+                    float prior_w, float* losses_out, float* logits_out, float* loss_out, void* ws, size_t ws_bytes,
+                    void* stream);
+int pso_db_loss_bwd(int loss_type, int B, int n, const void* eps, int eps_dtype, const float* noisy, const float* x0,
+                    const float* sigma, float beta, float neg_defactor, float prior_w, const float* grad_out,
+                    float grad_scale, void* deps, int deps_dtype, const void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * Implicit-GEMM 2-D convolution on NHWC bf16 images (fp32 accumulate).  weight is [Cout][ks][ks][C1+C2] (bf16).

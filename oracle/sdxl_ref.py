@@ -1,5 +1,5 @@
 """ORACLE (test infrastructure only) -- plain-PyTorch fp32 restatement of the diffusers 0.27.0 SDXL
-UNet2DConditionModel forward (+ peft LoRA) and AutoencoderKL decoder, reading diffusers-layout state dicts.
+UNet2DConditionModel forward (+ peft LoRA) and AutoencoderKL decoder / encoder, reading diffusers-layout state dicts.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.  It is the checker (and
 the CPU baseline), never the product.  diffusers/peft are not vendored in the reference and not installed here
@@ -162,6 +162,30 @@ def vae_decode(sd, z):
         i += 1
     h = F.silu(_gn(sd, "decoder.conv_norm_out", h, 1e-6))
     return _conv(sd, "decoder.conv_out", h)
+
+
+def vae_encode_moments(sd, x):
+    """AutoencoderKL.encode(x).latent_dist parameters: encoder -> quant_conv -> (mean, logvar clamped to [-30, 20]).
+    diffusers Encoder: the down-sampling convs pad (0, 1, 0, 1) then stride 2 with padding 0."""
+    h = _conv(sd, "encoder.conv_in", x)
+    i = 0
+    while f"encoder.down_blocks.{i}.resnets.0.norm1.weight" in sd:
+        j = 0
+        while f"encoder.down_blocks.{i}.resnets.{j}.norm1.weight" in sd:
+            h = resnet(sd, f"encoder.down_blocks.{i}.resnets.{j}", h, None, eps=1e-6)
+            j += 1
+        p = f"encoder.down_blocks.{i}.downsamplers.0.conv"
+        if p + ".weight" in sd:
+            h = F.conv2d(F.pad(h, (0, 1, 0, 1)), sd[p + ".weight"], sd[p + ".bias"], stride=2)
+        i += 1
+    h = resnet(sd, "encoder.mid_block.resnets.0", h, None, eps=1e-6)
+    h = vae_attention(sd, "encoder.mid_block.attentions.0", h)
+    h = resnet(sd, "encoder.mid_block.resnets.1", h, None, eps=1e-6)
+    h = F.silu(_gn(sd, "encoder.conv_norm_out", h, 1e-6))
+    h = _conv(sd, "encoder.conv_out", h)
+    h = _conv(sd, "quant_conv", h)
+    mean, logvar = h.chunk(2, dim=1)
+    return mean, logvar.clamp(-30.0, 20.0)
 
 
 def sd_to(sd, device, dtype=torch.float32):

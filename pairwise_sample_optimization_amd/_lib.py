@@ -36,6 +36,9 @@ SIGNATURES = {
     "pso_pair_loss_ws_bytes": (csz, [ci, ci]),
     "pso_pair_loss_fwd": (ci, [ci, ci, ci, vp, vp, vp, vp, ci, vp, vp, cf, cf, vp, vp, vp, csz, vp]),
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
+    "pso_db_loss_ws_bytes": (csz, [ci, ci]),
+    "pso_db_loss_fwd": (ci, [ci, ci, ci, vp, vp, ci, vp, vp, vp, cf, cf, cf, vp, vp, vp, vp, csz, vp]),
+    "pso_db_loss_bwd": (ci, [ci, ci, ci, vp, ci, vp, vp, vp, cf, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),

@@ -178,60 +178,89 @@ __global__ void gn_dparam_kernel(int B, int C, int nchunks, const float* __restr
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
 }
 
+// Apply passes: block = (pixel chunk of GN_ROWS, image) like the partial pass; thread (row slot, 8-channel chunk) folds
+// mean / rstd / gamma / beta of its 8 channels into per-channel (scale, shift) once and streams its pixel rows with
+// one FMA (+ SiLU) per element -- no per-element divisions or scalar parameter loads.
 template <bool SILU>
-__global__ void gn_apply_fwd_kernel(long nvec, int HW, int C, int G, const bf16_t* __restrict__ x,
-                                    const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
-                                    const bf16_t* __restrict__ beta, bf16_t* __restrict__ y) {
-  const int Cg = C / G, C8 = C / 8;
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-    const long pix = v / C8;
-    const int c0 = (int)(v - pix * C8) * 8;
-    const int b = (int)(pix / HW);
+__global__ void gn_apply_fwd_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const float* __restrict__ stats,
+                                    const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                    bf16_t* __restrict__ y) {
+  const int TPR = C / 8;
+  const int RS = blockDim.x / TPR;
+  const int slot = threadIdx.x / TPR, cc = threadIdx.x - slot * TPR;
+  if (slot >= RS) return;
+  const int b = blockIdx.y;
+  const int r0 = blockIdx.x * GN_ROWS, r1 = min(HW, r0 + GN_ROWS);
+  const int Cg = C / G;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cc * 8 + j, g = c / Cg;
+    const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
+    const float gm = gamma ? bf2f(gamma[c]) : 1.f, bt = beta ? bf2f(beta[c]) : 0.f;
+    sc[j] = rstd * gm;
+    sh[j] = bt - mean * rstd * gm;
+  }
+  for (int r = r0 + slot; r < r1; r += RS) {
+    const size_t off = ((size_t)b * HW + r) * C + cc * 8;
     float xv[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j, g = c / Cg;
-      const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
-      float z = (xv[j] - mean) * rstd;
-      z = z * (gamma ? bf2f(gamma[c]) : 1.f) + (beta ? bf2f(beta[c]) : 0.f);
+      const float z = fmaf(xv[j], sc[j], sh[j]);
       o[j] = SILU ? z * sigmoidf_(z) : z;
     }
-    *reinterpret_cast<uint4*>(y + v * 8) = pack8(o);
+    *reinterpret_cast<uint4*>(y + off) = pack8(o);
   }
 }
 
+// dx = rstd*(dz*gamma - ca - xhat*cb) (+ dadd), dz = dy * silu'(z) when SiLU is fused; per channel
+// xhat = x*rstd - mean*rstd, z = x*(rstd*gamma) + (beta - mean*rstd*gamma), dx = P*dz + Q + R*xhat.
 template <bool SILU>
-__global__ void gn_apply_bwd_kernel(long nvec, int HW, int C, int G, const bf16_t* __restrict__ x,
-                                    const bf16_t* __restrict__ dy, const float* __restrict__ stats,
-                                    const float* __restrict__ coef, const bf16_t* __restrict__ gamma,
-                                    const bf16_t* __restrict__ beta, const bf16_t* __restrict__ dadd,
-                                    bf16_t* __restrict__ dx) {
-  const int Cg = C / G, C8 = C / 8;
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-    const long pix = v / C8;
-    const int c0 = (int)(v - pix * C8) * 8;
-    const int b = (int)(pix / HW);
+__global__ void gn_apply_bwd_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                    const float* __restrict__ stats, const float* __restrict__ coef,
+                                    const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                    const bf16_t* __restrict__ dadd, bf16_t* __restrict__ dx) {
+  const int TPR = C / 8;
+  const int RS = blockDim.x / TPR;
+  const int slot = threadIdx.x / TPR, cc = threadIdx.x - slot * TPR;
+  if (slot >= RS) return;
+  const int b = blockIdx.y;
+  const int r0 = blockIdx.x * GN_ROWS, r1 = min(HW, r0 + GN_ROWS);
+  const int Cg = C / G;
+  float xs[8], xo[8], zs[8], zo[8], P[8], Q[8], R[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cc * 8 + j, g = c / Cg;
+    const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
+    const float ca = coef[(b * G + g) * 2], cb = coef[(b * G + g) * 2 + 1];
+    const float gm = gamma ? bf2f(gamma[c]) : 1.f, bt = beta ? bf2f(beta[c]) : 0.f;
+    xs[j] = rstd;
+    xo[j] = -mean * rstd;
+    zs[j] = rstd * gm;
+    zo[j] = bt - mean * rstd * gm;
+    P[j] = rstd * gm;
+    Q[j] = -rstd * ca;
+    R[j] = -rstd * cb;
+  }
+  for (int r = r0 + slot; r < r1; r += RS) {
+    const size_t off = ((size_t)b * HW + r) * C + cc * 8;
     float xv[8], dv[8], o[8], av[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
-    unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), dv);
-    if (dadd) unpack8(*reinterpret_cast<const uint4*>(dadd + v * 8), av);
+    unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+    unpack8(*reinterpret_cast<const uint4*>(dy + off), dv);
+    if (dadd) unpack8(*reinterpret_cast<const uint4*>(dadd + off), av);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j, g = c / Cg;
-      const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
-      const float ca = coef[(b * G + g) * 2], cb = coef[(b * G + g) * 2 + 1];
-      const float gm = gamma ? bf2f(gamma[c]) : 1.f;
-      const float xh = (xv[j] - mean) * rstd;
+      const float xh = fmaf(xv[j], xs[j], xo[j]);
       float dz = dv[j];
       if (SILU) {
-        const float z = xh * gm + (beta ? bf2f(beta[c]) : 0.f);
+        const float z = fmaf(xv[j], zs[j], zo[j]);
         const float sg = sigmoidf_(z);
         dz *= sg * (1.f + z * (1.f - sg));
       }
-      o[j] = rstd * (dz * gm - ca - xh * cb) + (dadd ? av[j] : 0.f);
+      o[j] = fmaf(P[j], dz, fmaf(R[j], xh, Q[j])) + (dadd ? av[j] : 0.f);
     }
-    *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
+    *reinterpret_cast<uint4*>(dx + off) = pack8(o);
   }
 }
 
@@ -242,11 +271,6 @@ static int gn_block(int C) {
   return TPR * rs;
 }
 
-static int grid_ew(long nvec) {
-  long g = (nvec + 255) / 256;
-  if (g > 4096) g = 4096;
-  return (int)(g < 1 ? 1 : g);
-}
 
 // ---------------------------------------------------------------------------------------------------------------
 // LayerNorm over the last dim (one wave per row).  MAXV = 16-B chunks per lane (C <= 64*8*MAXV).
@@ -369,13 +393,14 @@ int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, co
                                                                           nullptr, nullptr, nullptr, (float*)ws,
                                                                           nullptr);
   gn_finalize_kernel<false><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, eps, (const float*)ws, stats);
-  const long nvec = (long)B * HW * C / 8;
   if (silu)
-    gn_apply_fwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, (const bf16_t*)x, stats,
-                                                             (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y);
+    gn_apply_fwd_kernel<true><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, (const bf16_t*)x, stats,
+                                                                    (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                                    (bf16_t*)y);
   else
-    gn_apply_fwd_kernel<false><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, (const bf16_t*)x, stats,
-                                                              (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y);
+    gn_apply_fwd_kernel<false><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, (const bf16_t*)x, stats,
+                                                                     (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                                     (bf16_t*)y);
   return pso_check_launch("pso_group_norm_fwd");
 }
 
@@ -405,13 +430,12 @@ int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* d
   gn_finalize_kernel<true><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, coef);
   if (dgamma || dbeta)
     gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part_ch, dgamma, dbeta, accumulate_dparams);
-  const long nvec = (long)B * HW * C / 8;
   if (silu)
-    gn_apply_bwd_kernel<true><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, xp, dyp, stats, coef, gp, bp,
-                                                             (const bf16_t*)dadd, (bf16_t*)dx);
+    gn_apply_bwd_kernel<true><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, xp, dyp, stats, coef, gp, bp,
+                                                                    (const bf16_t*)dadd, (bf16_t*)dx);
   else
-    gn_apply_bwd_kernel<false><<<grid_ew(nvec), 256, 0, st>>>(nvec, HW, C, G, xp, dyp, stats, coef, gp, bp,
-                                                              (const bf16_t*)dadd, (bf16_t*)dx);
+    gn_apply_bwd_kernel<false><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, xp, dyp, stats, coef, gp, bp,
+                                                                     (const bf16_t*)dadd, (bf16_t*)dx);
   return pso_check_launch("pso_group_norm_bwd");
 }
 

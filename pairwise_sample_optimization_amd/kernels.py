@@ -225,6 +225,39 @@ def pair_loss_bwd(mode, x, x_prev, eps_pol, coef, pref, beta, clip_eps, ws, grad
     return deps
 
 
+DB_SIGMOID, DB_HINGE = 0, 1  # PSO_DB_* ("pso", "pso_db")
+
+
+def db_loss_ws(B, n, device):
+    return torch.empty(lib().pso_db_loss_ws_bytes(B, n), device=device, dtype=torch.uint8)
+
+
+def db_loss_fwd(loss_type, eps, noisy, x0, sigma, beta, neg_defactor, prior_w, ws, eps_ref=None):
+    """DreamBooth PSO loss (DB:1847-1935).  eps [2B,...] (instance rows first, negatives second), noisy / x0 fp32 of
+    the same shape, sigma fp32 [2B].  Returns (loss, per-image losses [2B or 4B], logits [B])."""
+    B2 = eps.shape[0]
+    n = eps[0].numel()
+    B = B2 // 2
+    losses = torch.empty((2 * B2 if eps_ref is not None else B2,), device=eps.device, dtype=torch.float32)
+    logits = torch.empty((B,), device=eps.device, dtype=torch.float32)
+    loss = torch.empty((), device=eps.device, dtype=torch.float32)
+    check(lib().pso_db_loss_fwd(loss_type, B, n, ptr(eps), ptr(eps_ref), dtype_code(eps), ptr(noisy), ptr(x0),
+                                ptr(sigma), float(beta), float(neg_defactor), float(prior_w), ptr(losses), ptr(logits),
+                                ptr(loss), ptr(ws), ws.numel(), stream_ptr()), "pso_db_loss_fwd")
+    return loss, losses, logits
+
+
+def db_loss_bwd(loss_type, eps, noisy, x0, sigma, beta, neg_defactor, prior_w, ws, grad_out=None, grad_scale=1.0,
+                out_dtype=BF16):
+    B = eps.shape[0] // 2
+    n = eps[0].numel()
+    deps = torch.empty(eps.shape, device=eps.device, dtype=out_dtype)
+    check(lib().pso_db_loss_bwd(loss_type, B, n, ptr(eps), dtype_code(eps), ptr(noisy), ptr(x0), ptr(sigma),
+                                float(beta), float(neg_defactor), float(prior_w), ptr(grad_out), float(grad_scale),
+                                ptr(deps), dtype_code(deps), ptr(ws), ws.numel(), stream_ptr()), "pso_db_loss_bwd")
+    return deps
+
+
 # ------------------------------------------------------------------------------------------------------------------
 # Norms
 # ------------------------------------------------------------------------------------------------------------------

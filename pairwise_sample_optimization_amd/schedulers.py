@@ -49,6 +49,42 @@ class EulerAncestralDiscreteScheduler:
             self.timesteps = self.timesteps.to(device)
 
 
+class EulerDiscreteScheduler:
+    """diffusers EulerDiscreteScheduler in its training configuration (no set_timesteps), as the DreamBooth trainer
+    loads it for EDM-style training (DB:1234-1237): timesteps 999..0, sigmas sqrt((1-abar)/abar) reversed + [0];
+    `add_noise(x0, noise, t) = x0 + noise * sigma(t)`; `get_sigmas` = DB:1675-1685."""
+
+    def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012):
+        self.num_train_timesteps = num_train_timesteps
+        self.alphas_cumprod = _alphas_cumprod(num_train_timesteps, beta_start, beta_end)
+        sig = np.array(((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5)
+        self.sigmas = torch.from_numpy(np.concatenate([sig[::-1], [0.0]]).astype(np.float32))
+        self.timesteps = torch.from_numpy(np.linspace(0, num_train_timesteps - 1, num_train_timesteps,
+                                                      dtype=np.float32)[::-1].copy())
+        self.config = type("Cfg", (), {"num_train_timesteps": num_train_timesteps, "prediction_type": "epsilon"})()
+
+    @classmethod
+    def from_pretrained(cls, *a, **kw):
+        return cls()
+
+    def sigma_at(self, t):
+        """sigma of integer timesteps t (any shape): sigmas[index of t in timesteps] = sigmas[999 - t].  Indexed on
+        t's device (a device-resident copy of the table), so the DreamBooth micro-step never syncs the host."""
+        t = torch.as_tensor(t).long()
+        if self.sigmas.device != t.device:
+            self._dev_sigmas = getattr(self, "_dev_sigmas", None)
+            if self._dev_sigmas is None or self._dev_sigmas.device != t.device:
+                self._dev_sigmas = self.sigmas.to(t.device)
+            return self._dev_sigmas[(self.num_train_timesteps - 1) - t]
+        return self.sigmas[(self.num_train_timesteps - 1) - t]
+
+
+def db_distill_timesteps(raw, distill_train_timesteps=4, num_train_timesteps=1000):
+    """DB:1769-1777: raw draws in [0, 1000) -> stride * (raw % steps) + stride - 1 ({249, 499, 749, 999} at 4)."""
+    stride = num_train_timesteps // distill_train_timesteps
+    return stride * (raw % distill_train_timesteps) + stride - 1
+
+
 class LCMScheduler:
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012):
         self.alphas_cumprod = _alphas_cumprod(num_train_timesteps, beta_start, beta_end)

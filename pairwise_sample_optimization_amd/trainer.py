@@ -70,6 +70,21 @@ def allreduce_grads(flat, process_group=None):
     return 1.0 / world
 
 
+def lora_optimizer_step(tr):
+    """accelerator.backward's sync step + clip_grad_norm_ + optimizer.step + zero_grad (T:857-861, DB:1953-1964) on
+    the flat LoRA bucket of tr.unet: RCCL all-reduce -> global-norm clip coefficient -> fused AdamW (clip and 1/world
+    folded into the gradient read) -> zero -> refresh the bf16 working copies.  tr carries exp_avg, exp_avg_sq,
+    opt_step, clip_buf, lr, betas, adam_eps, wd, max_grad_norm, pg."""
+    st = tr.unet.lora
+    scale = allreduce_grads(st.grad, tr.pg)
+    K.grad_clip_coef(st.grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
+    tr.opt_step += 1
+    K.adamw_step(st.master, st.grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
+                 grad_scale=scale, clip=tr.clip_buf)
+    K.zero_(st.grad)
+    st.refresh()
+
+
 class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
@@ -279,14 +294,7 @@ class PSOTrainer:
     # SYNC (T:857-861): all-reduce (RCCL) -> clip -> AdamW -> zero -> refresh bf16 working copies
     # ------------------------------------------------------------------------------------------------------------
     def optimizer_step(self):
-        st = self.unet.lora
-        scale = allreduce_grads(st.grad, self.pg)
-        K.grad_clip_coef(st.grad, self.max_grad_norm, grad_scale=scale, out=self.clip_buf)
-        self.opt_step += 1
-        K.adamw_step(st.master, st.grad, self.exp_avg, self.exp_avg_sq, self.lr, self.betas, self.adam_eps, self.wd,
-                     self.opt_step, grad_scale=scale, clip=self.clip_buf)
-        K.zero_(st.grad)
-        st.refresh()
+        lora_optimizer_step(self)
 
     def train_epoch(self, sb, generator=None):
         """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861), batched per accumulation

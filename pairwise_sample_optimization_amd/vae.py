@@ -1,4 +1,4 @@
-"""SDXL AutoencoderKL decoder (forward only) on the libpso_amd HIP kernels -- the reward-image decode of the sampler.
+"""SDXL AutoencoderKL decoder and encoder (forward only) on the libpso_amd HIP kernels -- the reward-image decode of the
 
 Drop-in surface: `vae.decode(z, return_dict=False)[0]`, `vae.config.scaling_factor`, diffusers
 state-dict keys (`post_quant_conv.*`, `decoder.*`; `encoder.*` / `quant_conv.*` of a full checkpoint are accepted and
@@ -10,6 +10,12 @@ GroupNorm eps 1e-6, 32 groups, no time embedding.
 
 All activations NHWC bf16.  The mid-block attention has head dim 512 (outside the d=64 flash kernel); its 16384 x 16384
 score matrix per image is small next to 288 GB, so it runs as GEMM (scores, bf16) -> row softmax -> GEMM.
+
+The encoder (the DreamBooth PSO step's `vae.encode(pixel_values).latent_dist.sample()`, DB:1750) is
+restated from diffusers 0.27.0 Encoder: conv_in (3->128) -> 4 DownEncoderBlock2D (2 resnets each; channels
+128,256,512,512; a stride-2 3x3 conv with (0,1,0,1) padding on the first three) -> mid (resnet, attention, resnet)
+-> GroupNorm+SiLU -> conv_out (2*latent) -> quant_conv (1x1) -> DiagonalGaussianDistribution (logvar clamped to
+[-30, 20]).
 """
 import math
 from dataclasses import dataclass
@@ -94,12 +100,72 @@ class Decoder(nn.Module):
         self.conv_out = Conv2d(ch[-1], cfg.out_channels, 3)
 
 
+class Downsample2DEnc(nn.Module):
+    """diffusers Downsample2D(use_conv=True, padding=0) of the encoder: F.pad(x, (0, 1, 0, 1)) then a stride-2 3x3
+    conv -- the bottom/right zero row/column are the conv gather's out-of-range taps."""
+
+    def __init__(self, C):
+        super().__init__()
+        self.conv = Conv2d(C, C, 3, stride=2)
+
+    def prepare(self):
+        self.conv.prepare()
+
+    def fwd(self, x):
+        B, H, W, C = x.shape
+        return K.conv2d(x, self.conv.w_nhwc, stride=2, pad=0, out_hw=(H // 2, W // 2), bias=self.conv.bias)
+
+
+class Encoder(nn.Module):
+    def __init__(self, cfg: VAEConfig):
+        super().__init__()
+        ch = list(cfg.block_out_channels)
+        G = cfg.norm_num_groups
+        self.conv_in = Conv2d(cfg.out_channels, ch[0], 3)
+        self.down_blocks = nn.ModuleList()
+        prev = ch[0]
+        for i, c in enumerate(ch):
+            blk = _Blk()
+            blk.resnets = nn.ModuleList([ResnetBlock2D(prev if j == 0 else c, c, G, 1e-6, 0)
+                                         for j in range(cfg.layers_per_block)])
+            if i < len(ch) - 1:
+                blk.downsamplers = nn.ModuleList([Downsample2DEnc(c)])
+            prev = c
+            self.down_blocks.append(blk)
+        mid = _Blk()
+        mid.resnets = nn.ModuleList([ResnetBlock2D(ch[-1], ch[-1], G, 1e-6, 0),
+                                     ResnetBlock2D(ch[-1], ch[-1], G, 1e-6, 0)])
+        mid.attentions = nn.ModuleList([VAEAttention(ch[-1], G)])
+        self.mid_block = mid
+        self.conv_norm_out = Norm(ch[-1])
+        self.conv_out = Conv2d(ch[-1], 2 * cfg.latent_channels, 3)
+
+
+class DiagonalGaussianDistribution:
+    """diffusers DiagonalGaussianDistribution over NCHW moments [mean | logvar] (logvar clamped to [-30, 20])."""
+
+    def __init__(self, mean, logvar):
+        self.mean = mean
+        self.logvar = logvar.clamp(-30.0, 20.0)
+        self.std = torch.exp(0.5 * self.logvar)
+        self.var = torch.exp(self.logvar)
+
+    def sample(self, generator=None):
+        noise = torch.randn(self.mean.shape, generator=generator, device=self.mean.device, dtype=self.mean.dtype)
+        return self.mean + self.std * noise
+
+    def mode(self):
+        return self.mean
+
+
 class AutoencoderKL(nn.Module):
     def __init__(self, config: VAEConfig = None):
         super().__init__()
         self.cfg = config or VAEConfig()
         self.config = SimpleNamespace(scaling_factor=self.cfg.scaling_factor,
                                       latent_channels=self.cfg.latent_channels)
+        self.encoder = Encoder(self.cfg)
+        self.quant_conv = Conv2d(2 * self.cfg.latent_channels, 2 * self.cfg.latent_channels, 1)
         self.post_quant_conv = Conv2d(self.cfg.latent_channels, self.cfg.latent_channels, 1)
         self.decoder = Decoder(self.cfg)
         self._prepared = False
@@ -113,7 +179,9 @@ class AutoencoderKL(nn.Module):
         return self
 
     def load_state_dict(self, sd, strict=True):
-        sd = {k: v.to(BF16) for k, v in sd.items() if not k.startswith(("encoder.", "quant_conv."))}
+        """diffusers AutoencoderKL keys (encoder.*, quant_conv.*, post_quant_conv.*, decoder.*).  A decoder-only
+        state dict loads with strict=False (the encoder keeps its init)."""
+        sd = {k: v.to(BF16) for k, v in sd.items()}
         res = super().load_state_dict(sd, strict=strict)
         self._prepared = False
         return res
@@ -121,8 +189,12 @@ class AutoencoderKL(nn.Module):
     def prepare(self):
         d = self.decoder
         for m in self.modules():
-            if isinstance(m, (ResnetBlock2D, Upsample2D, VAEAttention)):
+            if isinstance(m, (ResnetBlock2D, Upsample2D, VAEAttention, Downsample2DEnc)):
                 m.prepare()
+        e = self.encoder
+        e.conv_in.prepare()
+        e.conv_out.prepare()
+        self._qc_w = self.quant_conv.weight.data.reshape(self.quant_conv.cout, self.quant_conv.cin).contiguous()
         d.conv_in.prepare()
         lc = self.cfg.latent_channels
         self._lc_pad = 8 * ((lc + 7) // 8)
@@ -155,6 +227,40 @@ class AutoencoderKL(nn.Module):
         hn, _ = K.group_norm_fwd(x, d.conv_norm_out.weight, d.conv_norm_out.bias, self.cfg.norm_num_groups, 1e-6,
                                  True)
         return K.conv2d(hn, d.conv_out.w_nhwc, bias=d.conv_out.bias)
+
+    @torch.no_grad()
+    def encode_nhwc(self, x):
+        """x NCHW image in [-1, 1] (fp32 / bf16) -> moments NHWC fp32 [B, H/8, W/8, 2*latent] (mean | logvar)."""
+        if not self._prepared:
+            self.prepare()
+        e = self.encoder
+        B, _, H, W = x.shape
+        xh = K.nchw_to_nhwc(x)                                                    # [B,H,W,3] bf16
+        cols = K.im2col3(xh, e.conv_in.kp)
+        h = K.gemm(cols, e.conv_in.w_col, bias=e.conv_in.bias).view(B, H, W, -1)
+        rt = SimpleNamespace(save=False)
+        for blk in e.down_blocks:
+            for res in blk.resnets:
+                h = res.fwd(h, rt, None)
+            if hasattr(blk, "downsamplers"):
+                h = blk.downsamplers[0].fwd(h)
+        h = e.mid_block.resnets[0].fwd(h, rt, None)
+        h = e.mid_block.attentions[0].fwd(h)
+        h = e.mid_block.resnets[1].fwd(h, rt, None)
+        hn, _ = K.group_norm_fwd(h, e.conv_norm_out.weight, e.conv_norm_out.bias, self.cfg.norm_num_groups, 1e-6,
+                                 True)
+        mo = K.conv2d(hn, e.conv_out.w_nhwc, bias=e.conv_out.bias)              # [B,h,w,2L] bf16
+        _, h8, w8, L2 = mo.shape
+        return K.gemm(mo.view(-1, L2), self._qc_w, bias=self.quant_conv.bias,
+                      out_dtype=torch.float32).view(B, h8, w8, L2)
+
+    def encode(self, x, return_dict=True):
+        """diffusers `vae.encode(x).latent_dist` (DB:1750): NCHW fp32 moments in a DiagonalGaussianDistribution."""
+        mo = self.encode_nhwc(x)
+        L = self.cfg.latent_channels
+        mom = mo.permute(0, 3, 1, 2)
+        dist = DiagonalGaussianDistribution(mom[:, :L].contiguous(), mom[:, L:].contiguous())
+        return SimpleNamespace(latent_dist=dist) if return_dict else (dist,)
 
     def decode(self, z, return_dict=True):
         img = K.nhwc_to_nchw(self.decode_nhwc(z), torch.float32)
