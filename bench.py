@@ -89,8 +89,8 @@ def roofline(tr, buf, g):
     ms = sum(r[2].elapsed_time(r[3]) for r in rec)
     n = len(rec)
     achieved = fl / (ms * 1e-3) / 1e12
-    out = {"bound": "mfma", "kernel": "gemm_bf16_kernel<...> + gemm_tn_kernel (every GEMM / implicit-GEMM conv "
-                                      "launch of one train step)",
+    out = {"bound": "mfma", "kernel": "gemm_bf16_kernel<...> (incl. GEGLU fwd/bwd epilogues) + gemm_tn_rank_kernel "
+                                      "(every GEMM / implicit-GEMM conv / LoRA dW launch of one train step)",
            "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "launches_per_step": n,
            "flop_per_launch": fl / max(n, 1), "bytes_per_launch": nb / max(n, 1),

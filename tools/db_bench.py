@@ -1,0 +1,66 @@
+"""DreamBooth PSO micro-step throughput (BASELINE config 5 shape on one GPU: SDXL-Turbo UNet + SDXL VAE encoder,
+LoRA r=16, B=1 instance + 1 negative per micro-step, bf16; the fp8 forward of config 5 is not built -- DESIGN.md).
+Prints one JSON line.  usage: python tools/db_bench.py [--res 1024] [--steps 5] [--warmup 2] [--loss pso_db|pso]"""
+import argparse
+import json
+import os
+import sys
+import time
+from types import SimpleNamespace
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--rank", type=int, default=16)
+    ap.add_argument("--loss", default="pso_db")
+    a = ap.parse_args()
+    from pairwise_sample_optimization_amd.dreambooth import DreamBoothPSOTrainer
+    from pairwise_sample_optimization_amd.trainer import compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    from pairwise_sample_optimization_amd.vae import AutoencoderKL
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    h = a.res // 8
+    with torch.device(dev):
+        unet = UNet2DConditionModel(UNetConfig.sdxl(h))
+        vae = AutoencoderKL()
+    unet.init_weights(0)
+    vae.init_weights(1)
+    unet.add_adapter(SimpleNamespace(r=a.rank, lora_alpha=a.rank))
+    unet.lora.init_gaussian(seed=0, b_std=1e-3)
+    unet.prepare()
+    tr = DreamBoothPSOTrainer(unet, vae, loss_type=a.loss, beta_pso=5.0 if a.loss == "pso_db" else 200.0,
+                              gradient_accumulation_steps=4)
+    g = torch.Generator(device=dev).manual_seed(0)
+    B = a.batch
+    pix = torch.rand(2 * B, 3, a.res, a.res, device=dev, generator=g) * 2 - 1
+    enc = torch.randn(B, 77, 2048, device=dev, generator=g).bfloat16()
+    pooled = torch.randn(B, 1280, device=dev, generator=g).bfloat16()
+    tid = compute_time_ids(a.res, 0, dev).repeat(B, 1)
+    for _ in range(a.warmup):
+        tr.micro_step(pix, enc, pooled, tid, generator=g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.micro_step(pix, enc, pooled, tid, generator=g)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"metric": "DreamBooth PSO micro-step imgs/sec (instance + negative, SDXL-Turbo)",
+                      "value": round(2 * B / dt, 3), "unit": "imgs/s", "ms_per_step": round(dt * 1e3, 2),
+                      "n_gpus": 1, "steps": a.steps, "dtype": "bf16", "data": "synthetic",
+                      "config": {"workload": f"C5 (1 GPU, bf16 fwd): DreamBooth PSO {a.loss}, LoRA r={a.rank}, "
+                                             f"{B} instance + {B} negative, gas 4, VAE encode in the step",
+                                 "resolution": a.res},
+                      "loss": round(torch.stack(tr.loss_hist[-2:]).mean().item(), 6)}))
+
+
+if __name__ == "__main__":
+    main()
