@@ -81,9 +81,11 @@ def roofline(tr, buf, g):
     stream).  achieved = sum of algorithmic 2*M*N*K over those launches / sum of their durations."""
     from pairwise_sample_optimization_amd import kernels as K
     K.PROFILE = []
+    side, K.SideStream.enabled = K.SideStream.enabled, False  # serial launches: each event pair times one kernel alone
     one_step(tr, buf, g)
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
+    K.SideStream.enabled = side
     fl = sum(r[0] for r in rec)
     nb = sum(r[1] for r in rec)
     ms = sum(r[2].elapsed_time(r[3]) for r in rec)

@@ -305,6 +305,28 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = lane >> 4;
+  // Epilogue operands (bias, and the residual or the per-row-group bias) for the dense bf16/f32 store path, loaded into
+  // registers while the last K-tile computes instead of one dependent load per output subtile afterwards.
+  const bool epi_fast = EPI == EPI_NONE && MI * NJ <= 20 && gridDim.y == 1 && g.vec_ok && n0 + BN <= g.N && !(g.resid && g.rowbias);
+  uint2 ebias[NJ], eadd[MI][NJ];
+  auto epi_prefetch = [&]() {
+    if (!epi_fast) return;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
+      ebias[j] = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
+    }
+    const bf16_t* ap = g.resid ? g.resid : g.rowbias;
+    if (!ap) return;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(m0 + wm * (BM / WM) + i * 16 + fr, g.M - 1);
+      const long row = g.resid ? (long)m * g.ldr : (long)(m / g.rows_per_group) * g.ld_rowbias;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        eadd[i][j] = *reinterpret_cast<const uint2*>(ap + row + n0 + wn * (BN / WN) + j * 16 + fk * 4);
+    }
+  };
   if constexpr (PIPE) {
     // Register-pipelined schedule (2 LDS buffers + fragments of the next K-half in registers):
     //   iteration t:  ds_read kk=1 of tile t | MFMA kk=0 of t | lgkmcnt(0), vmcnt(0) [tile t+1 landed], s_barrier |
@@ -399,6 +421,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     // h and gate are rounded to bf16 first (the unfused path stores them in bf16 before the GEGLU).
     static_assert(NJ == 4, "GEGLU epilogue needs 64-column wave tiles");
     const int ng = n0 + wn * 64;
+    // the bias of this lane's 2 x 4 h / gate columns, loaded once up front (the stores below may alias it for the
+    // compiler, which would otherwise reload it per row subtile behind each store)
+    float bhv[2][4], bgv[2][4];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int nh = ng + jj * 16 + fk * 4;
+      const uint2 bh = *reinterpret_cast<const uint2*>(g.bias + nh);
+      const uint2 bg = *reinterpret_cast<const uint2*>(g.bias + nh + 32);
+      bhv[jj][0] = bf2f(bh.x & 0xffff); bhv[jj][1] = bf2f(bh.x >> 16); bhv[jj][2] = bf2f(bh.y & 0xffff); bhv[jj][3] = bf2f(bh.y >> 16);
+      bgv[jj][0] = bf2f(bg.x & 0xffff); bgv[jj][1] = bf2f(bg.x >> 16); bgv[jj][2] = bf2f(bg.y & 0xffff); bgv[jj][3] = bf2f(bg.y >> 16);
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = m0 + wm * (BM / WM) + i * 16 + fr;
@@ -407,14 +440,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       for (int jj = 0; jj < 2; ++jj) {
         const int nh = ng + jj * 16 + fk * 4;
         float vh[4], vg[4], o[4];
-        const uint2 bh = *reinterpret_cast<const uint2*>(g.bias + nh);
-        const uint2 bg = *reinterpret_cast<const uint2*>(g.bias + nh + 32);
-        const float bhv[4] = {bf2f(bh.x & 0xffff), bf2f(bh.x >> 16), bf2f(bh.y & 0xffff), bf2f(bh.y >> 16)};
-        const float bgv[4] = {bf2f(bg.x & 0xffff), bf2f(bg.x >> 16), bf2f(bg.y & 0xffff), bf2f(bg.y >> 16)};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          vh[r] = bf_round(acc[i][jj][r] * g.alpha + bhv[r]);
-          vg[r] = bf_round(acc[i][jj + 2][r] * g.alpha + bgv[r]);
+          vh[r] = bf_round(acc[i][jj][r] * g.alpha + bhv[jj][r]);
+          vg[r] = bf_round(acc[i][jj + 2][r] * g.alpha + bgv[jj][r]);
           o[r] = vh[r] * gelu_erf(vg[r]);
         }
         if (g.out2 && m < g.tail_m) {  // pre-activation rows kept for the backward (policy rows of a paired pass)
@@ -451,14 +480,30 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     {
       // dout chunk (row ml, columns c .. c+7 of the F-wide gradient) -> interleaved positions ph .. ph+7 (gate +32)
       constexpr int CC = BN / 8;
-      for (int q = threadIdx.x; q < BM * CC; q += NT) {
+      constexpr int ITERS = (BM * CC + NT - 1) / NT;
+      // every pre-activation load of this thread in flight at once (the output stores may alias them for the
+      // compiler, which would otherwise serialise one HBM round trip per chunk)
+      uint4 hvv[ITERS], gvv[ITERS];
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int q = threadIdx.x + it * NT;
+        const int ml = q / CC, cl = (q - (q / CC) * CC) * 8;
+        const int m = min(m0 + ml, g.M - 1), n = min(n0 + cl, g.N - 8);
+        const int ph = (n >> 5) * 64 + (n & 31);
+        if (q < BM * CC) {
+          hvv[it] = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph);
+          gvv[it] = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph + 32);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int q = threadIdx.x + it * NT;
         const int ml = q / CC, cl = (q - (q / CC) * CC) * 8;
         const int m = m0 + ml, n = n0 + cl;
-        if (m >= g.M || n >= g.N) continue;
+        if (q >= BM * CC || m >= g.M || n >= g.N) continue;
         const int ph = (n >> 5) * 64 + (n & 31);
         const uint4 dv = *reinterpret_cast<const uint4*>(tl + ml * TP + cl);
-        const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph);
-        const uint4 gv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph + 32);
+        const uint4 hv = hvv[it], gv = gvv[it];
         const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
         uint32_t oh[4], og[4];
 #pragma unroll
@@ -472,6 +517,38 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
         bf16_t* p = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
         *reinterpret_cast<uint4*>(p) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
         *reinterpret_cast<uint4*>(p + 32) = make_uint4(og[0], og[1], og[2], og[3]);
+      }
+    }
+    return;
+  }
+  if (!PIPE && epi_fast && nt > 0) {
+    epi_prefetch();  // every epilogue load in flight at once, then the arithmetic and the stores
+    const bool has_add = g.resid || g.rowbias;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + fr;
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
+        // same association as the generic path below: ((acc*alpha + bias) + rowbias | resid)
+        float v[4] = {acc[i][j][0] * g.alpha + bf2f(ebias[j].x & 0xffff), acc[i][j][1] * g.alpha + bf2f(ebias[j].x >> 16),
+                      acc[i][j][2] * g.alpha + bf2f(ebias[j].y & 0xffff), acc[i][j][3] * g.alpha + bf2f(ebias[j].y >> 16)};
+        if (has_add) {
+          v[0] += bf2f(eadd[i][j].x & 0xffff); v[1] += bf2f(eadd[i][j].x >> 16);
+          v[2] += bf2f(eadd[i][j].y & 0xffff); v[3] += bf2f(eadd[i][j].y >> 16);
+        }
+        if (g.out_dtype == PSO_BF16) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n) =
+              make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        } else {
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n);
+          if (g.accumulate) {
+            const float4 old = *o;
+            v[0] += old.x; v[1] += old.y; v[2] += old.z; v[3] += old.w;
+          }
+          *o = make_float4(v[0], v[1], v[2], v[3]);
+        }
       }
     }
     return;

@@ -4,6 +4,8 @@ Tensors are plain torch device tensors used as memory; every computation happens
 are channels-last bf16: linear inputs are [tokens, C] (any 2-D row-strided view), images are NHWC [B, H, W, C].
 There is no CPU / eager fallback: a missing library or a host tensor raises PsoLibError.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -30,6 +32,40 @@ def _prof_end(e0, flops, nbytes=0.0, tag=None):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         PROFILE.append((flops, nbytes, e0, e1, tag))
+
+
+class SideStream:
+    """Second HIP stream for launches off the critical path (the LoRA weight gradients of the backward): they only
+    accumulate into the flat fp32 grad buffer, so they can run beside the next input-gradient GEMMs and fill the CU
+    slots those leave (the dW kernels are latency-bound HBM streams).  `launch` orders the side stream after
+    everything the main stream has issued so far, and ties every tensor the launches read to the side stream
+    (caching-allocator record_stream), so no buffer is reused before they finish; `join` makes the main stream wait
+    for all of them (before the optimizer reads the grads).  Opt-in: PSO_SIDE_STREAM=1."""
+
+    enabled = os.environ.get("PSO_SIDE_STREAM", "0") == "1"  # measured neutral on the C2 step (31.35 vs 31.44 imgs/s)
+
+    def __init__(self):
+        self.s = None
+        self.pending = False
+
+    def launch(self, fn, *tensors):
+        if not self.enabled:
+            fn()
+            return
+        main = torch.cuda.current_stream()
+        if self.s is None:
+            self.s = torch.cuda.Stream(device=main.device)
+        self.s.wait_stream(main)
+        with torch.cuda.stream(self.s):
+            fn()
+        for t in tensors:
+            t.record_stream(self.s)
+        self.pending = True
+
+    def join(self):
+        if self.pending:
+            torch.cuda.current_stream().wait_stream(self.s)
+            self.pending = False
 
 
 def _row_stride(t):

@@ -409,8 +409,9 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_o2 = K.gemm(dh2, L.sBt_o2)
             da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=L.At_o2)
-            K.gemm_tn(v_o2, sv["a2"], g("attn2.A_o"))
-            K.gemm_tn(dh2, sv["u_o2"], g("attn2.B_o"), st.scale)
+            a2s, uo2 = sv["a2"], sv["u_o2"]
+            rt.side.launch(lambda: (K.gemm_tn(v_o2, a2s, g("attn2.A_o")), K.gemm_tn(dh2, uo2, g("attn2.B_o"), st.scale)),
+                           v_o2, a2s, dh2, uo2)
         else:
             da2 = K.gemm(dh2, o2.wt)
         enc = rt.enc
@@ -424,18 +425,21 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_q2 = K.gemm(dq2, L.sBt_q2)
             dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=L.At_q2)
-            K.gemm_tn(v_q2, sv["n2"], g("attn2.A_q"))
-            K.gemm_tn(dq2, sv["u_q2"], g("attn2.B_q"), st.scale)
-            # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
-            v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
-            K.gemm_tn(v_kv, rt.enc, g("attn2.A_kv"))
-            gB = g("attn2.B_kv")
-            u_kv2 = sv["u_kv2"]
-            if r in K.TN_RANKS:
-                K.gemm_tn(dkv2, u_kv2, gB, st.scale, group=C)
-            else:
-                K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
-                K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
+            n2s, uq2, enc_, u_kv2 = sv["n2"], sv["u_q2"], rt.enc, sv["u_kv2"]
+
+            def dw_attn2():
+                K.gemm_tn(v_q2, n2s, g("attn2.A_q"))
+                K.gemm_tn(dq2, uq2, g("attn2.B_q"), st.scale)
+                # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
+                v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
+                K.gemm_tn(v_kv, enc_, g("attn2.A_kv"))
+                gB = g("attn2.B_kv")
+                if r in K.TN_RANKS:
+                    K.gemm_tn(dkv2, u_kv2, gB, st.scale, group=C)
+                else:
+                    K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
+                    K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
+            rt.side.launch(dw_attn2, v_q2, n2s, dq2, uq2, dkv2, enc_, u_kv2)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
@@ -444,8 +448,9 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_o1 = K.gemm(dh1, L.sBt_o1)
             da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=L.At_o1)
-            K.gemm_tn(v_o1, sv["a1"], g("attn1.A_o"))
-            K.gemm_tn(dh1, sv["u_o1"], g("attn1.B_o"), st.scale)
+            a1s, uo1 = sv["a1"], sv["u_o1"]
+            rt.side.launch(lambda: (K.gemm_tn(v_o1, a1s, g("attn1.A_o")), K.gemm_tn(dh1, uo1, g("attn1.B_o"), st.scale)),
+                           v_o1, a1s, dh1, uo1)
         else:
             da1 = K.gemm(dh1, o1.wt)
         q3 = sv["qkv"].view(B, S, 3 * C)
@@ -456,15 +461,18 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             v_qkv = K.gemm_grouped_skinny(dqkv, L.sBt_qkv, 3)
             dn1 = K.gemm(dqkv, a1m.wt_qkv, a2=v_qkv, w2=L.At_qkv) if need_dx else None
-            K.gemm_tn(v_qkv, sv["n1"], g("attn1.A_qkv"))
-            gB = g("attn1.B_qkv")
-            u_qkv = sv["u_qkv"]
-            if r in K.TN_RANKS:
-                K.gemm_tn(dqkv, u_qkv, gB, st.scale, group=C)
-            else:
-                for j in range(3):
-                    K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
-                              st.scale)
+            n1s, u_qkv = sv["n1"], sv["u_qkv"]
+
+            def dw_attn1():
+                K.gemm_tn(v_qkv, n1s, g("attn1.A_qkv"))
+                gB = g("attn1.B_qkv")
+                if r in K.TN_RANKS:
+                    K.gemm_tn(dqkv, u_qkv, gB, st.scale, group=C)
+                else:
+                    for j in range(3):
+                        K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
+                                  st.scale)
+            rt.side.launch(dw_attn1, v_qkv, n1s, dqkv, u_qkv)
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv) if need_dx else None
         if not need_dx:  # first adapter block: nothing below it needs a gradient
@@ -787,7 +795,7 @@ class UNet2DConditionModel(nn.Module):
 
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
-        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False)
+        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=K.SideStream())
         rt.pol = lambda t: t[:t.shape[0] // 2] if rt.paired else t
         rt.lora = self.lora
         rt.r = self.lora.r if lora_on else 0
@@ -921,6 +929,7 @@ class UNet2DConditionModel(nn.Module):
                     dh = blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}")
                 dh = blk.resnets[j].bwd(dh, rt)
         rt.saved.clear()  # activations of the never-differentiated prefix
+        rt.side.join()  # LoRA weight gradients complete before anything reads lora.grad
         return None
 
     @property
