@@ -39,6 +39,18 @@ __device__ __forceinline__ s16x4 tr_read(const bf16_t* img, int r0, int col0, in
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off));
 }
 
+// The same read as inline asm, for kernels whose LDS ring is filled by LDS-DMA: hipcc cannot tell the builtin's LDS
+// read from the pending DMA writes and drains the ring (vmcnt(0)) before it.  The caller waits lgkmcnt itself.
+__device__ __forceinline__ s16x4 tr_read_asm(const bf16_t* img, int r0, int col0, int lane) {
+  const int li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = col0 + 4 * p;
+  const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(img + swz_tr(r0 + q, col >> 3) + (col & 7));
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
 __device__ __forceinline__ bf16x8 cat_frag(s16x4 a, s16x4 b) {
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
@@ -411,8 +423,13 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
           qa_[d2] = *reinterpret_cast<const bf16x8*>(sQr + swz_row(qs * 16 + c, d2 * 4 + g));
           oa_[d2] = *reinterpret_cast<const bf16x8*>(sOr + swz_row(qs * 16 + c, d2 * 4 + g));
         }
-        const float4 l4 = *reinterpret_cast<const float4*>(sL + qs * 16 + 4 * g);
-        const float4 d4 = *reinterpret_cast<const float4*>(sD + qs * 16 + 4 * g);
+        // LSE / delta through inline-asm LDS reads: as plain loads hipcc cannot tell them from the ring's pending
+        // LDS-DMA writes and drains the whole ring (vmcnt(0)), prefetch of the next query tile included
+        float4 l4, d4;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(l4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sL + qs * 16 + 4 * g)));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(d4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);  // nothing reads l4 / d4 (or moves above) before the wait
         float lq[4] = {l4.x * ln2inv, l4.y * ln2inv, l4.z * ln2inv, l4.w * ln2inv};
         const float dq_[4] = {d4.x, d4.y, d4.z, d4.w};
         if (qpart) {
@@ -436,16 +453,22 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         }
       }
       // dV^T[d][k] += dO^T . P ;  dK^T[d][k] += Q^T . dS
+      bf16x8 of[4], qf[4];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 of = cat_frag(tr_read(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
-                                   tr_read(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
-        const bf16x8 qf = cat_frag(tr_read(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
-                                   tr_read(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+        of[dt] = cat_frag(tr_read_asm(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
+                          tr_read_asm(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+        qf[dt] = cat_frag(tr_read_asm(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
+                          tr_read_asm(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll
         for (int kj = 0; kj < KJ; ++kj) {
-          dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pack_p(p[0][kj], p[1][kj]), dv[kj][dt], 0, 0, 0);
-          dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, pack_p(dsv[0][kj], dsv[1][kj]), dk[kj][dt], 0, 0, 0);
+          dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of[dt], pack_p(p[0][kj], p[1][kj]), dv[kj][dt], 0, 0, 0);
+          dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[dt], pack_p(dsv[0][kj], dsv[1][kj]), dk[kj][dt], 0, 0, 0);
         }
       }
     }

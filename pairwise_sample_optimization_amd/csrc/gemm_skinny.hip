@@ -12,6 +12,8 @@
 // group j multiplies A columns [j*K, (j+1)*K) with W columns [j*K, (j+1)*K) into out columns [j*N, (j+1)*N).
 #include "common.h"
 
+#include <cstdlib>
+
 __device__ __attribute__((aligned(16))) uint4 g_skinny_zero[4];  // source of every masked (K tail / N pad) load
 
 namespace {
@@ -19,12 +21,13 @@ namespace {
 constexpr int SK_W = 8;   // waves per workgroup (K split)
 
 // SK_MT 16-row MFMA tiles per wave (16*SK_MT rows per workgroup): 4 when M gives >= 256 workgroups, else 2
-template <int NJ, int SK_MT>
+template <int NJ, int SK_MT, int SK_U_ = 0>
 __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A,
                                                                    long lda, const bf16_t* __restrict__ W, long ldw,
                                                                    float alpha, void* __restrict__ out, long ldo,
                                                                    int out_f32, int accumulate) {
-  constexpr int SK_U = NJ <= 2 ? 4 : 2;  // K steps of loads in flight per wave (register budget: 2 waves / SIMD)
+  // K steps of loads in flight per wave (register budget: 2 waves / SIMD)
+  constexpr int SK_U = SK_U_ > 0 ? SK_U_ : ((NJ <= 2 && SK_MT <= 2) ? 4 : 2);
   __shared__ f32x4 red[SK_W][NJ][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = lane >> 4;
@@ -61,6 +64,9 @@ __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_nt_kernel(int M, int N,
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bfr[u][j] = *reinterpret_cast<const bf16x8*>((ok && wok[j]) ? wrow[j] + k : zero);
     }
+    // all SK_U steps' loads issued before the first MFMA: left alone, the scheduler interleaves them with the MFMAs
+    // under vmcnt(0) waits (two or three loads in flight per wave, one HBM round trip per K step)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < SK_U; ++u)
 #pragma unroll
@@ -101,9 +107,36 @@ __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_nt_kernel(int M, int N,
   }
 }
 
+// benchmark knob (PSO_SKINNY_VARIANT): 1 = 16-row tiles x 8 K steps in flight, 2 = 32-row x 8, 3 = 16-row x 4
+static int skinny_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PSO_SKINNY_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 template <int NJ>
 int launch_skinny(int M, int N, int K, const bf16_t* a, long lda, const bf16_t* w, long ldw, float alpha, void* out,
                   long ldo, int out_f32, int accumulate, int groups, hipStream_t st) {
+  const int var = NJ <= 2 ? skinny_variant() : 0;
+  if (var == 1 || var == 3) {
+    const dim3 grid((M + 15) / 16, groups);
+    if (var == 1)
+      gemm_skinny_nt_kernel<NJ, 1, 8><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                  accumulate);
+    else
+      gemm_skinny_nt_kernel<NJ, 1, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                  accumulate);
+    return pso_check_launch("pso_gemm(skinny)");
+  }
+  if (var == 2) {
+    const dim3 grid((M + 31) / 32, groups);
+    gemm_skinny_nt_kernel<NJ, 2, 8><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                accumulate);
+    return pso_check_launch("pso_gemm(skinny)");
+  }
   if ((long)((M + 63) / 64) * groups >= 256) {
     const dim3 grid((M + 63) / 64, groups);
     gemm_skinny_nt_kernel<NJ, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,

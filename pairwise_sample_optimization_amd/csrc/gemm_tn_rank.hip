@@ -29,7 +29,12 @@ __device__ __forceinline__ s16x4 tnr_tr(const bf16_t* img, int r0, int col0, int
   const int li = lane & 15;
   const int q = li >> 2, p = li & 3;
   const int col = col0 + 4 * p;
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((tnr_lds_s16x4*)(img + tnr_swz(r0 + q, col >> 3) + (col & 7)));
+  // inline asm: the builtin form is an LDS read the waitcnt pass cannot separate from the ring's pending LDS-DMA
+  // writes, so hipcc drains the whole ring (vmcnt(0)) before it.  The caller waits lgkmcnt itself.
+  const unsigned addr = (unsigned)(uintptr_t)(const tnr_lds_void*)(img + tnr_swz(r0 + q, col >> 3) + (col & 7));
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
 }
 __device__ __forceinline__ bf16x8 tnr_frag(const bf16_t* img, int m0, int col0, int lane) {
   typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -64,29 +69,60 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int
   const int prow = lane >> 3, pch = lane & 7;
   const int lc = pch ^ (2 * ((prow >> 1) & 3));  // logical source chunk of this lane's physical chunk
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_tnr_zero);
+  // Per-lane constant parts of the sources.  U padding columns (col >= R) read the zero chunk at row stride 0, so
+  // a full 64-row step issues its pieces with no per-lane predicate: exec-masked loads would make hipcc wrap every
+  // glds in a branch and drain the ring with vmcnt(0) before the LDS reads.  Only the ragged last step (M % 64)
+  // takes the predicated path.
+  static_assert((UIMG * 8) % 4 == 0, "U pieces split evenly over the 4 waves");
+  const bf16_t* xsrc[4];
+  int xdst[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int xi = piece >> 3, pr = piece & 7;
+    xsrc[i] = X + (long)(pr * 8 + prow) * ldx + c0 + xi * 64 + lc * 8;
+    xdst[i] = xi * TNR_IMG + pr * 8 * 64;
+  }
+  constexpr int UP = UIMG * 8 / 4;
+  const bf16_t* usrc[UP];
+  long ustr[UP];
+  int udst[UP], urow[UP];
+#pragma unroll
+  for (int i = 0; i < UP; ++i) {
+    const int piece = wave + 4 * i;
+    const int ui = piece >> 3, pr = piece & 7;
+    const int col = ui * 64 + lc * 8;
+    const bool ok = col < R;
+    urow[i] = pr * 8 + prow;
+    usrc[i] = ok ? U + (long)urow[i] * ldu + u_off + col : zero;
+    ustr[i] = ok ? ldu : 0;
+    udst[i] = (2 + ui) * TNR_IMG + pr * 8 * 64;
+  }
   auto issue = [&](int st, int buf) {
     bf16_t* base = lds + buf * STAGE;
-    // X: pieces 0..15 = (image xi = piece / 8, rows (piece % 8) * 8 ..); wave w issues pieces 4w .. 4w+3
+    const long m0 = (long)st * 64;
+    if (m0 + 64 <= M) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = wave * 4 + i;
-      const int xi = piece >> 3, pr = piece & 7;
-      const int m = st * 64 + pr * 8 + prow;
-      const bf16_t* src = m < M ? X + (long)m * ldx + c0 + xi * 64 + lc * 8 : zero;
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src), (tnr_lds_void*)(base + xi * TNR_IMG + pr * 8 * 64),
-                                       16, 0, 0);
-    }
-    // U: UIMG images x 8 pieces, dealt round-robin over the waves
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(xsrc[i] + m0 * ldx), (tnr_lds_void*)(base + xdst[i]),
+                                         16, 0, 0);
 #pragma unroll
-    for (int i = 0; i < (UIMG * 8 + 3) / 4; ++i) {
-      const int piece = wave + 4 * i;
-      if (piece < UIMG * 8) {
-        const int ui = piece >> 3, pr = piece & 7;
-        const int m = st * 64 + pr * 8 + prow;
-        const int col = ui * 64 + lc * 8;
-        const bf16_t* src = (m < M && col < R) ? U + (long)m * ldu + u_off + col : zero;
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(src),
-                                         (tnr_lds_void*)(base + (2 + ui) * TNR_IMG + pr * 8 * 64), 16, 0, 0);
+      for (int i = 0; i < UP; ++i)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(usrc[i] + m0 * ustr[i]),
+                                         (tnr_lds_void*)(base + udst[i]), 16, 0, 0);
+    } else {  // ragged last step: rows past M read the zero chunk
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int piece = wave * 4 + i;
+        const bool ok = m0 + (piece & 7) * 8 + prow < M;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? xsrc[i] + m0 * ldx : zero),
+                                         (tnr_lds_void*)(base + xdst[i]), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < UP; ++i) {
+        const bool ok = m0 + urow[i] < M;
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? usrc[i] + m0 * ustr[i] : zero),
+                                         (tnr_lds_void*)(base + udst[i]), 16, 0, 0);
       }
     }
   };
@@ -115,6 +151,8 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int
       for (int ci = 0; ci < 2; ++ci) xf[ci] = tnr_frag(ximg, ks * 32, xcol + ci * 16, lane);
 #pragma unroll
       for (int j = 0; j < NJT; ++j) uf[j] = tnr_frag(base + (2 + (j >> 2)) * TNR_IMG, ks * 32, (j & 3) * 16, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs behind the wait (hipcc moves register-only ops past asm)
 #pragma unroll
       for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
