@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--num-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each epoch as one captured hipGraph (measured neutral: 31.32 vs 31.36 imgs/s eager)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
@@ -71,9 +73,13 @@ def build(args, dev):
     return unet, tr, buf, g
 
 
-def one_step(tr, buf, g):
+def one_step(tr, buf, g, graph=False):
+    """shuffle (eager: a few gathers) + one epoch; graph=True replays the epoch's captured hipGraph."""
     sb = tr.shuffle(buf, generator=g)
-    tr.train_epoch(sb)
+    if graph:
+        tr.train_epoch_graph(sb)
+    else:
+        tr.train_epoch(sb)
 
 
 def roofline(tr, buf, g):
@@ -156,14 +162,14 @@ def main():
     unet, tr, buf, g = build(args, dev)
     log(f"[bench] built + sampled in {time.time() - t_build:.1f}s; warmup {args.warmup}")
     for _ in range(args.warmup):
-        one_step(tr, buf, g)
+        one_step(tr, buf, g, graph=args.graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_step(tr, buf, g)
+        one_step(tr, buf, g, graph=args.graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -183,7 +189,7 @@ def main():
                                "%d-step sampler (T=%d)" % (args.rank, args.pairs, args.gas, args.num_steps,
                                                            args.num_steps - 1),
                    "global_batch": 2 * args.pairs * world, "seq_len": (args.res // 16) ** 2, "resolution": args.res,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "launch": "hipgraph-epoch" if args.graph else "eager"},
         "loss": round(loss, 6),
     }
     tf = SURVEY_TFLOP_PER_PAIR_MICRO.get(args.rank) if args.res == 1024 else None

@@ -504,9 +504,12 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 //   dP^T = V . dO^T ; dS^T = P^T * (dP^T - delta) ; dQ^T[d][q] += K^T . dS^T  (K^T via transposed reads)
 // ================================================================================================================
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sKr[ATT_KT * ATT_D];
-  __shared__ __attribute__((aligned(16))) bf16_t sKt[ATT_KT * ATT_D];
-  __shared__ __attribute__((aligned(16))) bf16_t sVr[ATT_KT * ATT_D];
+  // K/V tiles arrive by LDS-DMA through a 3-stage ring (two tiles in flight behind a counted vmcnt, one barrier per
+  // tile) as three images per stage: K row image, K transposed-read image, V row image (source-side swizzles).
+  constexpr int STG = 3;
+  constexpr int PIECES = 6;  // glds per wave per tile: 2 pieces x 3 images
+  constexpr int IMG = ATT_KT * ATT_D;
+  __shared__ __attribute__((aligned(16))) bf16_t sRing[STG][3][IMG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
@@ -542,16 +545,35 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     for (int dt = 0; dt < 4; ++dt) dq[qi][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (a.Sk + ATT_KT - 1) / ATT_KT;
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcR = pch ^ prow;                     // row-image source chunk (swz_row)
+  const int lcT = pch ^ (2 * ((prow >> 1) & 3));  // transposed-read image source chunk (swz_tr)
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int pw = 0; pw < 2; ++pw) {
+      const int piece = wave * 2 + pw;
+      const int key = min(kt * ATT_KT + piece * 8 + prow, a.Sk - 1);  // clamped rows are masked (p = 0)
+      const bf16_t* krow = K + (long)key * a.ldk;
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(krow + lcR * 8),
+                                       (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(krow + lcT * 8),
+                                       (att_lds_void*)(sRing[buf][1] + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(V + (long)key * a.ldv + lcR * 8),
+                                       (att_lds_void*)(sRing[buf][2] + piece * 8 * ATT_D), 16, 0, 0);
+    }
+  };
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
   for (int kt = 0; kt < nkt; ++kt) {
+    // tile kt landed (all but this wave's PIECES youngest), then every wave's; the barrier also orders every wave's
+    // reads of tile kt-1 before its buffer is re-staged below
+    if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % STG);
+    const bf16_t* sKr = sRing[kt % STG][0];
+    const bf16_t* sKt = sRing[kt % STG][1];
+    const bf16_t* sVr = sRing[kt % STG][2];
     const int kbase = kt * ATT_KT;
-    uint4 rk[2], rv[2];
-    stage_load(rk, K, a.ldk, kbase, a.Sk, tid);
-    stage_load(rv, V, a.ldv, kbase, a.Sk, tid);
-    __syncthreads();
-    stage_store<false>(rk, sKr, tid);
-    stage_store<true>(rk, sKt, tid);
-    stage_store<false>(rv, sVr, tid);
-    __syncthreads();
     f32x4 dsT[2][4];  // lane holds dS[q = qi*16 + c][key = kj*16 + 4g + r]
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {

@@ -657,6 +657,12 @@ int pso_gemm_skinny_nt(int M, int N, int K, const void* A, long lda, const void*
 int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long ldu, int R, int group_c, float alpha,
                      float* out, long ldo, int out_jc, hipStream_t st);
 
+// 8-phase 256x256 kernel (gemm8p.hip): dense A . W^T (+ bias) -> bf16, and the GEGLU-epilogue form
+int pso_gemm8p(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias, void* out,
+               long ldo, int group_m, hipStream_t st);
+int pso_gemm8p_geglu(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
+                     void* out, long ldo, void* out_pre, long ld_pre, int pre_rows, int group_m, hipStream_t st);
+
 static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
@@ -691,6 +697,13 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if (ks < 1) ks = 1;
     return launch<64, 64>(g, st, (int)ks);
   }
+  // 8-phase 256x256 (variant 30 forces it where it applies): dense bf16 out, optional bias, K % 128 == 0
+  const bool ok8 = !g.conv.mode && !g.a2 && !g.rowbias && !g.resid && g.out_dtype == PSO_BF16 && !g.accumulate &&
+                   g.alpha == 1.f && (g.N % 256) == 0 && (g.K1 % 128) == 0 && g.vec_ok && al16(g.a1) && al16(g.b1) &&
+                   (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 && (long)g.M * g.lda1 < (1L << 30) &&
+                   (long)g.N * g.ldb1 < (1L << 30);
+  if (g_gemm_variant == 30 && ok8)
+    return pso_gemm8p(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.bias, g.out, g.ldo, g.group_m, st);
   if (g_gemm_variant == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (g_gemm_variant == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (g_gemm_variant == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
@@ -929,6 +942,11 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   g.tail_m = (pre_rows > 0 && pre_rows < M) ? pre_rows : M;
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  // variant 32: the 8-phase kernel (gemm8p.hip; K % 128 == 0).  Measured equal on the UNet GEGLU shapes (16384 x
+  // 10240 x 1280: 877 vs 879 TF/s; 65536 x 5120 x 640: 701 vs 697), so the 2-phase 256x256 kernel stays the default.
+  if (g_gemm_variant == 32 && (K % 128) == 0 && (long)M * lda < (1L << 30) && (long)N * ldw < (1L << 30))
+    return pso_gemm8p_geglu(M, N, K, a, lda, w, ldw, bias, out, ldo, out_pre, ld_pre, g.tail_m, g.group_m,
+                            (hipStream_t)stream);
   return launch<256, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
 }
 

@@ -296,6 +296,50 @@ class PSOTrainer:
     def optimizer_step(self):
         lora_optimizer_step(self)
 
+    _SB_TENSORS = ("x", "x_next", "unet_in", "enc", "pooled", "tid", "t", "coef", "rewards")
+
+    def train_epoch_graph(self, sb, generator=None):
+        """train_epoch as ONE hipGraph replay (torch.cuda.CUDAGraph over the HIP runtime): the epoch's micro-steps --
+        paired UNet pass, fused loss, backward into the flat LoRA grad bucket -- are captured on the first call and
+        replayed afterwards, so the ~7k kernel launches of an epoch cost one graph launch instead of one host call
+        each.  The shuffled buffer is copied into the graph's static input buffers first; the optimizer step (its
+        AdamW step count is a host scalar) runs eagerly after the replay.  Requires: the epoch is exactly one
+        accumulation window starting at a window boundary, and the turbo sampler draws no reward column (m = 1);
+        otherwise this is train_epoch."""
+        if (sb.n_micro != self.gas_total or self.n_micro % self.gas_total or not self.auto_step
+                or (self.mode == MODE_TURBO and self.m > 1)):
+            return self.train_epoch(sb, generator)
+        key = tuple((k, tuple(getattr(sb, k).shape)) for k in self._SB_TENSORS)
+        g = getattr(self, "_graph", None)
+        if g is None or self._graph_key != key:
+            self._graph = None
+            self._gsb = SimpleNamespace(n_micro=sb.n_micro, P=sb.P,
+                                        **{k: getattr(sb, k).clone() for k in self._SB_TENSORS})
+            st = self.unet.lora
+            saved = st.grad.clone()
+            self.auto_step = False
+            n0, h0 = self.n_micro, len(self.loss_hist)
+            try:
+                self.train_epoch(self._gsb)  # eager warm-up of everything the capture will launch
+                torch.cuda.synchronize()
+                h1 = len(self.loss_hist)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.train_epoch(self._gsb)
+                self._gloss = self.loss_hist[h1:]
+            finally:
+                self.auto_step = True
+                self.n_micro = n0
+                del self.loss_hist[h0:]
+                st.grad.copy_(saved)
+            self._graph, self._graph_key = g, key
+        for k in self._SB_TENSORS:
+            getattr(self._gsb, k).copy_(getattr(sb, k))
+        self._graph.replay()
+        self.loss_hist.extend(l.clone() for l in self._gloss)
+        self.n_micro += sb.n_micro
+        self.optimizer_step()
+
     def train_epoch(self, sb, generator=None):
         """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861), batched per accumulation
         window up to `max_pass_images` images per UNet pass."""

@@ -191,6 +191,28 @@ def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
         K_.lib().pso_gemm_set_variant(0)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 2560, 1280), (1000, 768, 640), (300, 256, 128), (16384, 1024, 256),
+                                   (257, 512, 384)])
+def test_gemm_8phase(cuda, M, N, K):
+    """The 8-phase 256x256 kernel (gemm8p.hip, variant 30): bias epilogue, ragged last row tile, 2..20 K-tiles
+    (odd and even K-tile pair counts); nothing is written past the output rows."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(30)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        b = torch.randn(N, device=cuda, generator=g).bfloat16()
+        ref = a.float() @ w.float().t() + b.float()
+        sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+        out = sentinel[:M]
+        K_.gemm(a, w, bias=b, out=out)
+        assert _rel(out, ref) < 4e-3
+        assert (sentinel[M:] == 7.0).all()
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19])
 def test_conv_every_variant_large(cuda, variant):
     from pairwise_sample_optimization_amd import kernels as K_

@@ -114,9 +114,19 @@ def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("variant", [0, 32])  # 0: 2-phase 256x256 kernel; 32: the 8-phase kernel where K % 128 == 0
 @pytest.mark.parametrize("M,dim", [(8192, 1280), (300, 64), (1000, 640)])
-def test_gemm_geglu_fused(cuda, M, dim):
+def test_gemm_geglu_fused(cuda, M, dim, variant):
     """GEGLU in the GEMM epilogue (interleaved weight rows) and its backward fused into the dout GEMM, vs torch fp32."""
+    from pairwise_sample_optimization_amd import kernels as K
+    K.lib().pso_gemm_set_variant(variant)
+    try:
+        _geglu_case(cuda, M, dim)
+    finally:
+        K.lib().pso_gemm_set_variant(0)
+
+
+def _geglu_case(cuda, M, dim):
     from pairwise_sample_optimization_amd import kernels as K
     Fd = 4 * dim
     g = torch.Generator(device="cuda").manual_seed(M + dim)

@@ -203,3 +203,47 @@ def test_batched_window_equals_sequential_micro_steps(cuda, mode):
     with pytest.raises(ValueError):
         tr.n_micro = 1
         tr.micro_step(tr.micro_batch(sb, 0, sb.n_micro))
+
+
+def test_graph_epoch_equals_eager_epoch(cuda):
+    """train_epoch_graph (the epoch captured once as a hipGraph, then replayed with fresh shuffled inputs) leaves the
+    same LoRA parameters, AdamW moments and losses as the eager train_epoch over the same shuffles."""
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+    P, gas = 2, 2
+
+    def make():
+        with torch.device(cuda):
+            unet = UNet2DConditionModel(cfg)
+        unet.init_weights(0)
+        unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+        unet.lora.init_gaussian(seed=1, b_std=0.05)
+        unet.prepare()
+        return unet, PSOTrainer(unet, mode="turbo", num_steps=2, gradient_accumulation_steps=gas,
+                                train_batch_size=P, lr=1e-3)
+
+    u_e, tr_e = make()
+    u_g, tr_g = make()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Bp = P * gas
+    enc = torch.randn(Bp, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(Bp, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(128, 0, cuda).repeat(Bp, 1)
+    buf = tr_e.sample_pairs(enc, pooled, tid, 16, generator=g,
+                            reward_fn=lambda x: torch.rand(x.shape[0], device=cuda, generator=g))
+    for epoch in range(3):  # capture on the first call, replay on the next two (different shuffles)
+        sb = tr_e.shuffle(buf, generator=torch.Generator(device="cuda").manual_seed(100 + epoch))
+        tr_e.train_epoch(sb)
+        tr_g.train_epoch_graph(sb)
+    torch.cuda.synchronize()
+    assert tr_g._graph is not None and tr_g.opt_step == tr_e.opt_step == 3
+    le = torch.stack(tr_e.loss_hist).cpu()
+    lg = torch.stack(tr_g.loss_hist).cpu()
+    assert torch.allclose(le, lg, rtol=1e-5, atol=1e-6), (le, lg)
+    # the LoRA dW kernels accumulate with float atomics, so grads agree to rounding, not bitwise; AdamW turns a
+    # rounding difference on a near-zero gradient into up to ~lr of parameter change: bar 1 % of lr = 1e-5
+    assert torch.allclose(u_e.lora.master, u_g.lora.master, rtol=0, atol=1e-5), \
+        (u_e.lora.master - u_g.lora.master).abs().max().item()
+    for a, b in ((tr_e.exp_avg, tr_g.exp_avg), (tr_e.exp_avg_sq, tr_g.exp_avg_sq)):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-9), (a - b).abs().max().item()

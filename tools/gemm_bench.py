@@ -47,6 +47,13 @@ def run(dev):
         ref = a.float() @ w.float().t()
         err = ((K.gemm(a, w).float() - ref).norm() / ref.norm()).item()
         rows.append((name, f"{M}x{N}x{Kd} e={err:.1e}", ms, 2 * M * N * Kd / ms / 1e9))
+    for (M, F, Kd, name) in [(2 * L2, 5120, 1280, "L2x2 geglu"), (2 * L1, 2560, 640, "L1x2 geglu")]:
+        a = torch.randn(M, Kd, device=dev).bfloat16()
+        w = (torch.randn(2 * F, Kd, device=dev) / Kd ** 0.5).bfloat16()
+        b = torch.randn(2 * F, device=dev).bfloat16()
+        pre = torch.empty(M // 2, 2 * F, device=dev, dtype=torch.bfloat16)
+        ms = t_ms(lambda: K.gemm_geglu(a, w, b, out_pre=pre, pre_rows=M // 2))
+        rows.append((name, f"{M}x{2 * F}x{Kd}", ms, 2 * M * 2 * F * Kd / ms / 1e9))
     for (B, H, Ci, Co, name, mode) in [(Bi, 128, 320, 320, "L0 conv 320", K.CONV_NORMAL),
                                        (Bi, 64, 640, 640, "L1 conv 640", K.CONV_NORMAL),
                                        (Bi, 32, 1280, 1280, "L2 conv 1280", K.CONV_NORMAL),
