@@ -232,6 +232,23 @@ int pso_silu(long n, const void* x, void* y, void* stream);
 int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, int out_col, void* stream);
 int pso_transpose(int R, int Rp, int C, const void* in, long ldi, void* out, long ldo, void* stream);
 int pso_im2col3(int B, int H, int W, int C, const void* in, void* out, int Kp, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * Full-UNet weight gradients (BASELINE C3 / C4, SURVEY §8a a6 "full dW in C3 (build-only)"; the reference trains LoRA
+ * only, App. A #4).  The dW products run on pso_gemm_tn; these supply the rest:
+ * pso_colsum_acc: out[g][n] += sum over rows m in [g*rows_per_group, (g+1)*rows_per_group) of x[m][n] (bf16 in, f32
+ *   out; bias gradients with rows_per_group = M, per-image time-embedding row-bias gradients with rows_per_group = HW).
+ * pso_layer_norm_dparam: dgamma[c] += sum_m dy[m][c] (x[m][c] - mean_m) rstd_m; dbeta[c] += sum_m dy[m][c] (stats
+ *   from pso_layer_norm_fwd).  torch LayerNorm weight / bias grads.
+ * pso_im2col_conv: 3x3 patch matrix [B*Ho*Wo][9*(C1+C2)] in the NHWC weight order (tap-major, channel-minor) for mode
+ *   PSO_CONV_NORMAL (stride 1 / 2) or PSO_CONV_UP2 (nearest 2x upsample), sources concatenated on channels; zero
+ *   padding.  dW[Cout][3][3][Cin] = dY^T . cols (torch conv2d weight grad).
+ * ------------------------------------------------------------------------------------------------------------------ */
+int pso_colsum_acc(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* stream);
+int pso_layer_norm_dparam(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                          float* dgamma, float* dbeta, void* stream);
+int pso_im2col_conv(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+                    int stride, int pad, void* out, long ldo, void* stream);
 int pso_sumpool2(int B, int H, int W, int C, const void* in, const void* dadd, void* out, void* stream);
 int pso_axpby(long n, float a, const void* x, float b, const void* z, void* y, void* stream);
 int pso_cast_f32_bf16(long n, const float* x, float scale, void* y, void* stream);

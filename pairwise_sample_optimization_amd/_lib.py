@@ -66,6 +66,9 @@ SIGNATURES = {
     "pso_timestep_embedding": (ci, [ci, ci, vp, vp, cl, ci, vp]),
     "pso_transpose": (ci, [ci, ci, ci, vp, cl, vp, cl, vp]),
     "pso_im2col3": (ci, [ci, ci, ci, ci, vp, vp, ci, vp]),
+    "pso_colsum_acc": (ci, [cl, ci, vp, cl, cl, vp, cl, vp]),
+    "pso_layer_norm_dparam": (ci, [ci, ci, vp, cl, vp, cl, vp, vp, vp, vp]),
+    "pso_im2col_conv": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, vp, cl, vp]),
     "pso_sumpool2": (ci, [ci, ci, ci, ci, vp, vp, vp, vp]),
     "pso_axpby": (ci, [cl, cf, vp, cf, vp, vp, vp]),
     "pso_cast_f32_bf16": (ci, [cl, vp, cf, vp, vp]),

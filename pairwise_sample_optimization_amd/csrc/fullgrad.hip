@@ -1,0 +1,157 @@
+// Weight-gradient helpers for full-UNet training (BASELINE config C3/C4, SURVEY §8a a6 "full dW in C3").
+//
+// The reference trains LoRA only; C3 asks the build for gradients of every UNet parameter (App. A #4).  The dW GEMMs
+// themselves run on the TN GEMM (gemm.hip pso_gemm_tn); these kernels supply what they need around it:
+//   pso_colsum_acc         out[g][n] += sum of x[m][n] over the rows m of group g (bias gradients: one group; the
+//                          per-image time-embedding row-bias gradients of the resnets: one group per image)
+//   pso_layer_norm_dparam  dgamma[c] += sum_m dy[m][c] * (x[m][c] - mean_m) * rstd_m,  dbeta[c] += sum_m dy[m][c]
+//   pso_im2col_conv        the 3x3 patch matrix [B*Ho*Wo][9*(C1+C2)] (tap-major, channel-minor: the NHWC weight
+//                          layout [Cout][kh][kw][Cin]) of a NORMAL (stride 1/2) or UP2 (nearest 2x upsample) conv over
+//                          one or two concatenated NHWC sources, so dW = dY^T . cols is one TN GEMM.
+#include "common.h"
+
+namespace {
+
+constexpr int CS_ROWS = 256;  // rows per colsum / dparam workgroup
+
+// 256 threads = 4 row slices x 64 column quads; each block covers 256 rows x 256 columns
+__global__ __launch_bounds__(256) void colsum_kernel(long M, int N, const bf16_t* __restrict__ x, long ldx, long rpg,
+                                                     float* __restrict__ out, long ldo) {
+  const int t = threadIdx.x;
+  const int n = (blockIdx.x * 64 + (t & 63)) * 4;
+  const long r0 = (long)blockIdx.y * CS_ROWS;
+  const long r1 = min(M, r0 + CS_ROWS);
+  if (n >= N) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  long cur = r0 / rpg;
+  for (long m = r0 + (t >> 6); m < r1; m += 4) {
+    const long gm = m / rpg;
+    if (gm != cur) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) atomicAdd(out + cur * ldo + n + r, s[r]);
+      s[0] = s[1] = s[2] = s[3] = 0.f;
+      cur = gm;
+    }
+    if (n + 4 <= N) {
+      const uint2 v = *reinterpret_cast<const uint2*>(x + m * ldx + n);
+      s[0] += bf2f(v.x & 0xffff); s[1] += bf2f(v.x >> 16); s[2] += bf2f(v.y & 0xffff); s[3] += bf2f(v.y >> 16);
+    } else {
+      for (int r = 0; r < 4 && n + r < N; ++r) s[r] += bf2f(x[m * ldx + n + r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (n + r < N) atomicAdd(out + cur * ldo + n + r, s[r]);
+}
+
+__global__ __launch_bounds__(256) void ln_dparam_kernel(int M, int C, const bf16_t* __restrict__ x, long ldx,
+                                                        const bf16_t* __restrict__ dy, long lddy,
+                                                        const float* __restrict__ stats, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
+  const int t = threadIdx.x;
+  const int c = (blockIdx.x * 64 + (t & 63)) * 4;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(M, r0 + CS_ROWS);
+  if (c >= C) return;
+  float g[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int m = r0 + (t >> 6); m < r1; m += 4) {
+    const float mean = stats[2 * m], rstd = stats[2 * m + 1];
+    const uint2 xv = *reinterpret_cast<const uint2*>(x + (long)m * ldx + c);
+    const uint2 dv = *reinterpret_cast<const uint2*>(dy + (long)m * lddy + c);
+    const float xs[4] = {bf2f(xv.x & 0xffff), bf2f(xv.x >> 16), bf2f(xv.y & 0xffff), bf2f(xv.y >> 16)};
+    const float ds[4] = {bf2f(dv.x & 0xffff), bf2f(dv.x >> 16), bf2f(dv.y & 0xffff), bf2f(dv.y >> 16)};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      g[r] += ds[r] * (xs[r] - mean) * rstd;
+      b[r] += ds[r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    atomicAdd(dgamma + c + r, g[r]);
+    atomicAdd(dbeta + c + r, b[r]);
+  }
+}
+
+// one thread per (output pixel, tap, 8-channel chunk)
+__global__ __launch_bounds__(256) void im2col_conv_kernel(int mode, int B, const bf16_t* __restrict__ s1, int C1,
+                                                          const bf16_t* __restrict__ s2, int C2, int H, int W, int Ho,
+                                                          int Wo, int stride, int pad, bf16_t* __restrict__ out,
+                                                          long ldo) {
+  const int Ct = C1 + C2, nch = Ct / 8;
+  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long total = (long)B * Ho * Wo * 9 * nch;
+  if (idx >= total) return;
+  const int ch = (int)(idx % nch);
+  const long rest = idx / nch;
+  const int tap = (int)(rest % 9);
+  const long p = rest / 9;
+  const int ox = (int)(p % Wo);
+  const int oy = (int)((p / Wo) % Ho);
+  const int b = (int)(p / ((long)Wo * Ho));
+  const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+  int iy, ix;
+  bool ok;
+  if (mode == PSO_CONV_UP2) {
+    const int uy = oy + ky - pad, ux = ox + kx - pad;
+    ok = (unsigned)uy < (unsigned)(2 * H) && (unsigned)ux < (unsigned)(2 * W);
+    iy = uy >> 1;
+    ix = ux >> 1;
+  } else {
+    iy = oy * stride + ky - pad;
+    ix = ox * stride + kx - pad;
+    ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+  }
+  const int c = ch * 8;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (ok) {
+    const long pix = ((long)b * H + iy) * W + ix;
+    v = c < C1 ? *reinterpret_cast<const uint4*>(s1 + pix * C1 + c)
+               : *reinterpret_cast<const uint4*>(s2 + pix * C2 + (c - C1));
+  }
+  *reinterpret_cast<uint4*>(out + p * ldo + (long)tap * Ct + c) = v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pso_colsum_acc(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && N > 0 && x && out && rows_per_group > 0, "pso_colsum_acc: bad arguments");
+  PSO_ARG_CHECK((((uintptr_t)x) & 7) == 0 && (ldx % 4) == 0, "pso_colsum_acc: 8-B aligned rows");
+  if (M == 0) return PSO_OK;
+  const dim3 grid((N + 255) / 256, (unsigned)((M + CS_ROWS - 1) / CS_ROWS));
+  colsum_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, N, (const bf16_t*)x, ldx, rows_per_group, out, ldo);
+  return pso_check_launch("pso_colsum_acc");
+}
+
+int pso_layer_norm_dparam(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                          float* dgamma, float* dbeta, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && C > 0 && (C % 4) == 0 && x && dy && stats && dgamma && dbeta,
+                "pso_layer_norm_dparam: bad arguments (C % 4 == 0)");
+  PSO_ARG_CHECK((((uintptr_t)x) & 7) == 0 && (((uintptr_t)dy) & 7) == 0 && (ldx % 4) == 0 && (lddy % 4) == 0,
+                "pso_layer_norm_dparam: 8-B aligned rows");
+  if (M == 0) return PSO_OK;
+  const dim3 grid((C + 255) / 256, (M + CS_ROWS - 1) / CS_ROWS);
+  ln_dparam_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
+                                                         dgamma, dbeta);
+  return pso_check_launch("pso_layer_norm_dparam");
+}
+
+int pso_im2col_conv(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+                    int stride, int pad, void* out, long ldo, void* stream) {
+  PSO_ARG_CHECK(B > 0 && src1 && out && C1 > 0 && (C1 % 8) == 0 && (C2 % 8) == 0 && (!C2 || src2) &&
+                    (mode == PSO_CONV_NORMAL || mode == PSO_CONV_UP2) && ldo >= 9L * (C1 + C2) && (ldo % 8) == 0,
+                "pso_im2col_conv: bad arguments (C1, C2 % 8 == 0; NORMAL or UP2; ldo >= 9 (C1 + C2))");
+  PSO_ARG_CHECK((((uintptr_t)src1) & 15) == 0 && (!src2 || (((uintptr_t)src2) & 15) == 0) &&
+                    (((uintptr_t)out) & 15) == 0,
+                "pso_im2col_conv: 16-B aligned buffers");
+  const long total = (long)B * Ho * Wo * 9 * ((C1 + C2) / 8);
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  im2col_conv_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(mode, B, (const bf16_t*)src1, C1, (const bf16_t*)src2,
+                                                              C2, H, W, Ho, Wo, stride, pad, (bf16_t*)out, ldo);
+  return pso_check_launch("pso_im2col_conv");
+}
+
+}  // extern "C"

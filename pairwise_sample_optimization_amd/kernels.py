@@ -453,6 +453,35 @@ def axpby(a, x, b=0.0, z=None, out=None):
     return out
 
 
+def colsum_acc(x, out, rows_per_group=None):
+    """out [G, N] f32 += per-group column sums of x [M, N] bf16 (G = M / rows_per_group; bias / row-bias grads)."""
+    M, N = x.shape
+    rpg = M if rows_per_group is None else rows_per_group
+    check(lib().pso_colsum_acc(M, N, ptr(x), _row_stride(x), rpg, ptr(out), out.stride(0) if out.dim() > 1 else N,
+                               stream_ptr()), "pso_colsum_acc")
+    return out
+
+
+def layer_norm_dparam(x, dy, stats, dgamma, dbeta):
+    """dgamma / dbeta [C] f32 += LayerNorm weight / bias grads (stats from layer_norm_fwd)."""
+    M, C = x.shape
+    check(lib().pso_layer_norm_dparam(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats),
+                                      ptr(dgamma), ptr(dbeta), stream_ptr()), "pso_layer_norm_dparam")
+
+
+def im2col_conv(x, x2=None, mode=CONV_NORMAL, stride=1, pad=1, out_hw=None):
+    """3x3 patch matrix [B*Ho*Wo, 9*(C1+C2)] (tap-major, channel-minor) of an NHWC conv input (+ concat source)."""
+    B, H, W, C1 = x.shape
+    C2 = x2.shape[3] if x2 is not None else 0
+    if out_hw is None:
+        out_hw = (2 * H, 2 * W) if mode == CONV_UP2 else ((H + 2 * pad - 3) // stride + 1, (W + 2 * pad - 3) // stride + 1)
+    Ho, Wo = out_hw
+    out = torch.empty((B * Ho * Wo, 9 * (C1 + C2)), device=x.device, dtype=BF16)
+    check(lib().pso_im2col_conv(mode, B, ptr(x.contiguous()), C1, ptr(x2.contiguous()) if x2 is not None else None, C2,
+                                H, W, Ho, Wo, stride, pad, ptr(out), out.stride(0), stream_ptr()), "pso_im2col_conv")
+    return out
+
+
 def add(x, z):
     return axpby(1.0, x, 1.0, z)
 

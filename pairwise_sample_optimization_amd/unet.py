@@ -148,6 +148,63 @@ class Norm(nn.Module):
 
 
 # ======================================================================================================================
+# Full-UNet training state (BASELINE C3 / C4, SURVEY §8a a6 "full dW in C3 (build-only)")
+# ======================================================================================================================
+class FullGradState:
+    """Every UNet parameter trainable (the reference always trains LoRA -- App. A #4 -- so this is the build-only C3 /
+    C4 mode).  ONE flat fp32 master (initialised from the bf16 module weights) and ONE flat fp32 grad (the all-reduce
+    bucket / optimizer operand) in named_parameters order, with a per-parameter view of each; the module parameters
+    stay the bf16 working copies the kernels read, rewritten from the master by refresh() (then the kernel-layout
+    caches are rebuilt by UNet2DConditionModel.prepare())."""
+
+    def __init__(self, unet):
+        params = [p for _, p in unet.named_parameters()]
+        n = sum(p.numel() for p in params)
+        dev = params[0].device
+        self.params = params
+        self.master = torch.empty(n, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=dev, dtype=torch.float32)
+        self._g, self._m = {}, {}
+        off = 0
+        for p in params:
+            k = p.numel()
+            self._m[id(p)] = self.master[off:off + k].view(p.shape)
+            self._g[id(p)] = self.grad[off:off + k].view(p.shape)
+            self._m[id(p)].copy_(p.data.float())
+            off += k
+        self.numel = n
+        self.trigger = torch.zeros(1, device=dev, requires_grad=True)  # autograd hook for UNet.forward (_UNetFn)
+
+    def g(self, p):
+        """fp32 gradient view of module parameter p (same shape)."""
+        return self._g[id(p)]
+
+    def refresh(self):
+        """master -> bf16 module weights (the caller re-runs prepare())."""
+        with torch.no_grad():
+            for p in self.params:
+                p.data.copy_(self._m[id(p)])
+
+
+def _lin_dw(fg, lin, dy, x):
+    """nn.Linear weight / bias grads: dW += dy^T x (TN GEMM), db += column sums of dy."""
+    K.gemm_tn(dy, x, fg.g(lin.weight))
+    if lin.bias is not None:
+        K.colsum_acc(dy, fg.g(lin.bias).view(1, -1))
+
+
+def _conv_dw(fg, conv, dy2d, cols):
+    """3x3 conv weight / bias grads from the patch matrix cols [M, 9*Cin] (tap-major): dW_nhwc = dy^T cols, then
+    into the diffusers [Cout][Cin][kh][kw] grad view."""
+    tmp = torch.zeros((dy2d.shape[1], cols.shape[1]), device=cols.device, dtype=torch.float32)
+    K.gemm_tn(dy2d, cols, tmp)
+    co = conv.cout
+    fg.g(conv.weight).add_(tmp[:co, :9 * conv.cin].view(co, 3, 3, conv.cin).permute(0, 3, 1, 2))
+    if conv.bias is not None:
+        K.colsum_acc(dy2d[:, :co] if dy2d.shape[1] != co else dy2d, fg.g(conv.bias).view(1, -1))
+
+
+# ======================================================================================================================
 # LoRA state: flat fp32 masters + flat fp32 grads (the all-reduce bucket), bf16 working copies
 # ======================================================================================================================
 class LoraState:
@@ -386,6 +443,8 @@ class BasicTransformerBlock(nn.Module):
                       st3=pol(st3), f=f)
             if lo:
                 sv.update(u_qkv=u_qkv, u_o1=u_o1, u_q2=u_q2, u_kv2=u_kv2, u_o2=u_o2)
+            if rt.fg is not None:  # full-UNet grads: the ff.proj / ff.out inputs too
+                sv.update(n3=n3, gg=gg)
             rt.saved.append(sv)
         return h3
 
@@ -401,8 +460,21 @@ class BasicTransformerBlock(nn.Module):
         g = (lambda k: st.grad_seg(path, k)) if lo else None
         a1m, a2m = self.attn1, self.attn2
         # --- FF ---
+        fg = rt.fg
         df = K.gemm_geglu_bwd(dh3, self.ff.out.wt, sv["f"])  # interleaved d[h | gate]
+        if fg is not None:
+            _lin_dw(fg, self.ff.out, dh3, sv["gg"])
+            F2 = df.shape[1]
+            idx = K.geglu_interleave_index(F2 // 2, df.device)
+            tmp = torch.zeros((F2, C), device=df.device, dtype=torch.float32)
+            K.gemm_tn(df, sv["n3"], tmp)
+            fg.g(self.ff.proj.weight).index_add_(0, idx, tmp)
+            tb = torch.zeros((1, F2), device=df.device, dtype=torch.float32)
+            K.colsum_acc(df, tb)
+            fg.g(self.ff.proj.bias).index_add_(0, idx, tb[0])
         dn3 = K.gemm(df, self.ff.wt_int)
+        if fg is not None:
+            K.layer_norm_dparam(sv["h2"], dn3, sv["st3"], fg.g(self.norm3.weight), fg.g(self.norm3.bias))
         dh2 = K.layer_norm_bwd(sv["h2"], dn3, sv["st3"], self.norm3.weight, dadd=dh3)
         # --- cross attention out-proj:  y = a W^T + (a A^T)(sB)^T ;  v = dy sB ; da = dy W + v A ---
         o2 = a2m.to_out[0]
@@ -414,6 +486,8 @@ class BasicTransformerBlock(nn.Module):
                            v_o2, a2s, dh2, uo2)
         else:
             da2 = K.gemm(dh2, o2.wt)
+        if fg is not None:
+            _lin_dw(fg, o2, dh2, sv["a2"])
         enc = rt.enc
         Se = enc.shape[0] // B
         kv3 = sv["kv2"].view(B, Se, 2 * C)
@@ -442,6 +516,11 @@ class BasicTransformerBlock(nn.Module):
             rt.side.launch(dw_attn2, v_q2, n2s, dq2, uq2, dkv2, enc_, u_kv2)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
+        if fg is not None:
+            K.gemm_tn(dq2, sv["n2"], fg.g(a2m.to_q.weight))
+            K.gemm_tn(dkv2[:, :C], enc, fg.g(a2m.to_k.weight))
+            K.gemm_tn(dkv2[:, C:], enc, fg.g(a2m.to_v.weight))
+            K.layer_norm_dparam(sv["h1"], dn2, sv["st2"], fg.g(self.norm2.weight), fg.g(self.norm2.bias))
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
         # --- self attention ---
         o1 = a1m.to_out[0]
@@ -453,6 +532,8 @@ class BasicTransformerBlock(nn.Module):
                            v_o1, a1s, dh1, uo1)
         else:
             da1 = K.gemm(dh1, o1.wt)
+        if fg is not None:
+            _lin_dw(fg, o1, dh1, sv["a1"])
         q3 = sv["qkv"].view(B, S, 3 * C)
         dqkv = torch.empty((M, 3 * C), device=dh3.device, dtype=BF16)
         d3 = dqkv.view(B, S, 3 * C)
@@ -475,6 +556,10 @@ class BasicTransformerBlock(nn.Module):
             rt.side.launch(dw_attn1, v_qkv, n1s, dqkv, u_qkv)
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv) if need_dx else None
+        if fg is not None:
+            for j, lin in enumerate((a1m.to_q, a1m.to_k, a1m.to_v)):
+                K.gemm_tn(dqkv[:, j * C:(j + 1) * C], sv["n1"], fg.g(lin.weight))
+            K.layer_norm_dparam(sv["x"], dn1, sv["st1"], fg.g(self.norm1.weight), fg.g(self.norm1.bias))
         if not need_dx:  # first adapter block: nothing below it needs a gradient
             return None
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
@@ -525,14 +610,19 @@ class Transformer2DModel(nn.Module):
         xn, st = K.group_norm_fwd(x, self.norm.weight, self.norm.bias, self.groups, 1e-6, False)
         h = K.gemm(xn.view(-1, C), self.proj_in.weight, bias=self.proj_in.bias)
         if rt.save:
-            rt.saved.append({"x": rt.pol(x), "st": rt.pol(st)})
+            rt.saved.append({"x": rt.pol(x), "st": rt.pol(st), "xn": xn.view(-1, C) if rt.fg is not None else None})
         for i, blk in enumerate(self.transformer_blocks):
             h = blk.fwd(h, rt, f"{path}.transformer_blocks.{i}")
+        if rt.save and rt.fg is not None:
+            rt.saved.append({"hout": h})
         return K.gemm(h, self.proj_out.weight, bias=self.proj_out.bias, resid=x.view(-1, C)).view(B, H, W, C)
 
     def bwd(self, dy, rt, path, need_dx=True):
         B, H, W, C = dy.shape
         d2 = dy.view(-1, C)
+        fg = rt.fg
+        if fg is not None:
+            _lin_dw(fg, self.proj_out, d2, rt.saved.pop()["hout"])
         dh = K.gemm(d2, self.proj_out.wt)
         for i in reversed(range(len(self.transformer_blocks))):
             dh = self.transformer_blocks[i].bwd(dh, rt.saved.pop(), rt, f"{path}.transformer_blocks.{i}",
@@ -541,6 +631,10 @@ class Transformer2DModel(nn.Module):
         if not need_dx:
             return None
         dn = K.gemm(dh, self.proj_in.wt).view(B, H, W, C)
+        if fg is not None:
+            _lin_dw(fg, self.proj_in, dh, sv["xn"])
+            return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy,
+                                    dgamma=fg.g(self.norm.weight), dbeta=fg.g(self.norm.bias), accumulate=True)
         return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy)
 
 
@@ -574,19 +668,39 @@ class ResnetBlock2D(nn.Module):
             sc = x
         out = K.conv2d(h2, self.conv2.w_nhwc, bias=self.conv2.bias, resid=sc)
         if rt.save:
-            rt.saved.append({"x": rt.pol(x), "st1": rt.pol(st1), "c1": rt.pol(c1), "st2": rt.pol(st2)})
+            sv = {"x": rt.pol(x), "st1": rt.pol(st1), "c1": rt.pol(c1), "st2": rt.pol(st2)}
+            if rt.fg is not None:  # conv inputs for the weight grads
+                sv.update(h1=h1, h2=h2)
+            rt.saved.append(sv)
         return out
 
     def bwd(self, dout, rt):
         sv = rt.saved.pop()
+        fg = rt.fg
+        B, H, W, _ = dout.shape
         dh2 = K.conv2d(dout, self.conv2.w_dx)
-        dc1 = K.group_norm_bwd(sv["c1"], dh2, sv["st2"], self.norm2.weight, self.norm2.bias, True)
+        if fg is not None:
+            _conv_dw(fg, self.conv2, dout.view(-1, self.cout), K.im2col_conv(sv["h2"]))
+            dc1 = K.group_norm_bwd(sv["c1"], dh2, sv["st2"], self.norm2.weight, self.norm2.bias, True,
+                                   dgamma=fg.g(self.norm2.weight), dbeta=fg.g(self.norm2.bias), accumulate=True)
+            dc2 = dc1.view(-1, self.cout)
+            _conv_dw(fg, self.conv1, dc2, K.im2col_conv(sv["h1"]))
+            # time-embedding row bias (one row per image): per-image column sums -> the time_emb_proj output grad
+            K.colsum_acc(dc2, rt.dtemb[:, self._temb_off:self._temb_off + self.cout], rows_per_group=H * W)
+        else:
+            dc1 = K.group_norm_bwd(sv["c1"], dh2, sv["st2"], self.norm2.weight, self.norm2.bias, True)
         dh1 = K.conv2d(dc1, self.conv1.w_dx)
         if self.conv_shortcut is not None:
-            B, H, W, _ = dout.shape
             dsc = K.gemm(dout.view(-1, self.cout), self.conv_shortcut.wt).view(B, H, W, self.cin)
+            if fg is not None:
+                K.gemm_tn(dout.view(-1, self.cout), sv["x"].view(-1, self.cin),
+                          fg.g(self.conv_shortcut.weight).view(self.cout, self.cin))
+                K.colsum_acc(dout.view(-1, self.cout), fg.g(self.conv_shortcut.bias).view(1, -1))
         else:
             dsc = dout
+        if fg is not None:
+            return K.group_norm_bwd(sv["x"], dh1, sv["st1"], self.norm1.weight, self.norm1.bias, True, dadd=dsc,
+                                    dgamma=fg.g(self.norm1.weight), dbeta=fg.g(self.norm1.bias), accumulate=True)
         return K.group_norm_bwd(sv["x"], dh1, sv["st1"], self.norm1.weight, self.norm1.bias, True, dadd=dsc)
 
 
@@ -600,11 +714,13 @@ class Downsample2D(nn.Module):
 
     def fwd(self, x, rt):
         if rt.save:
-            rt.saved.append({"hw": x.shape[1:3]})
+            rt.saved.append({"hw": x.shape[1:3], "x": x if rt.fg is not None else None})
         return K.conv2d(x, self.conv.w_nhwc, stride=2, bias=self.conv.bias)
 
     def bwd(self, dy, rt):
         sv = rt.saved.pop()
+        if rt.fg is not None:
+            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout), K.im2col_conv(sv["x"], stride=2))
         return K.conv2d(dy, self.conv.w_dx, mode=K.CONV_T2, out_hw=tuple(sv["hw"]))
 
 
@@ -617,9 +733,14 @@ class Upsample2D(nn.Module):
         self.conv.prepare()
 
     def fwd(self, x, rt):
+        if rt.save and rt.fg is not None:
+            rt.saved.append({"x": x})
         return K.conv2d(x, self.conv.w_nhwc, mode=K.CONV_UP2, bias=self.conv.bias)
 
     def bwd(self, dy, rt):
+        if rt.fg is not None:
+            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout),
+                     K.im2col_conv(rt.saved.pop()["x"], mode=K.CONV_UP2))
         du = K.conv2d(dy, self.conv.w_dx)  # input-gradient on the 2x grid
         return K.sumpool2(du)
 
@@ -707,6 +828,7 @@ class UNet2DConditionModel(nn.Module):
         self.conv_norm_out = Norm(ch[0])
         self.conv_out = Conv2d(ch[0], cfg.out_channels, 3)
         self.lora = None
+        self.full = None  # FullGradState when every parameter is trained (C3 / C4)
         self._adapters_enabled = True
         self._prepared = False
         self.gradient_checkpointing = False
@@ -761,6 +883,20 @@ class UNet2DConditionModel(nn.Module):
         self._adapters_enabled = True
         return self.lora
 
+    def enable_full_grads(self):
+        """Train every UNet parameter (BASELINE C3 / C4; the reference has no such path, App. A #4): flat fp32
+        master + grad over named_parameters; backward_nhwc then accumulates every weight gradient into self.full.grad
+        and runs down to conv_in.  Adapters, if any, must be absent."""
+        if self.lora is not None:
+            raise ValueError("full-UNet training and LoRA adapters are exclusive")
+        self.full = FullGradState(self)
+        return self.full
+
+    def refresh_full(self):
+        """After an optimizer step on self.full.master: bf16 module weights + kernel-layout caches."""
+        self.full.refresh()
+        self.prepare()
+
     def disable_adapters(self):
         self._adapters_enabled = False
 
@@ -786,6 +922,11 @@ class UNet2DConditionModel(nn.Module):
         self._temb_n = off
         self.conv_in.prepare()
         self.conv_out.prepare()
+        if self.full is not None:
+            self._temb_wt = K.transpose(self._temb_w)  # [tdim][sum Co]: input gradient of the batched projection
+            for lin in (self.time_embedding.linear_1, self.time_embedding.linear_2, self.add_embedding.linear_1,
+                        self.add_embedding.linear_2):
+                lin.prepare()
         self._prepared = True
         if self.lora is not None:
             self.refresh_lora()
@@ -795,7 +936,8 @@ class UNet2DConditionModel(nn.Module):
 
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
-        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=K.SideStream())
+        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=K.SideStream(),
+                             fg=self.full if save else None)
         rt.pol = lambda t: t[:t.shape[0] // 2] if rt.paired else t
         rt.lora = self.lora
         rt.r = self.lora.r if lora_on else 0
@@ -808,12 +950,18 @@ class UNet2DConditionModel(nn.Module):
             t = t.expand(B).contiguous()
         te = K.timestep_embedding(t, cfg.time_proj_dim)
         l1, l2 = self.time_embedding.linear_1, self.time_embedding.linear_2
-        emb = K.gemm(K.silu(K.gemm(te, l1.weight, bias=l1.bias)), l2.weight, bias=l2.bias)
+        t1 = K.gemm(te, l1.weight, bias=l1.bias)
+        s1 = K.silu(t1)
+        emb = K.gemm(s1, l2.weight, bias=l2.bias)
         tid = K.timestep_embedding(time_ids.reshape(-1), cfg.addition_time_embed_dim).view(B, -1)
         add_in = K.concat_channels(text_embeds.to(BF16).contiguous(), tid)
         a1, a2 = self.add_embedding.linear_1, self.add_embedding.linear_2
-        emb = K.gemm(K.silu(K.gemm(add_in, a1.weight, bias=a1.bias)), a2.weight, bias=a2.bias, resid=emb)
-        return K.gemm(K.silu(emb), self._temb_w, bias=self._temb_b)  # [B, sum Co]
+        u1 = K.gemm(add_in, a1.weight, bias=a1.bias)
+        s2 = K.silu(u1)
+        emb = K.gemm(s2, a2.weight, bias=a2.bias, resid=emb)
+        se = K.silu(emb)
+        self._emb_saved = dict(te=te, t1=t1, s1=s1, add_in=add_in, u1=u1, s2=s2, emb=emb, se=se)
+        return K.gemm(se, self._temb_w, bias=self._temb_b)  # [B, sum Co]
 
     def forward_nhwc(self, x, timestep, enc, text_embeds, time_ids, save=False, paired_ref=False):
         """Core forward.  x NHWC bf16 [B,h,w,4]; enc [B,77,Dc]; returns eps NHWC bf16 [B,h,w,4].
@@ -837,7 +985,15 @@ class UNet2DConditionModel(nn.Module):
         h = K.gemm(cols, self.conv_in.w_col, bias=self.conv_in.bias).view(B, H, W, -1)
         skips = [h]
         i0, j0 = self._first_attn
-        rt.save = False  # the prefix below the first adapter block is never differentiated (backward_nhwc)
+        full = rt.fg is not None
+        if full and paired_ref:
+            raise ValueError("full-UNet training: the reference is a separate frozen UNet, not the adapter-free pass")
+        if full:
+            rt.emb = self._emb_saved
+            rt.cols_in = cols
+            i0, j0 = -1, -1  # everything is differentiated: no adapter-free prefix
+        else:
+            rt.save = False  # the prefix below the first adapter block is never differentiated (backward_nhwc)
         for i, blk in enumerate(self.down_blocks):
             for j, res in enumerate(blk.resnets):
                 if (i, j) == (i0, j0):  # entering the adapter-carrying part
@@ -876,7 +1032,7 @@ class UNet2DConditionModel(nn.Module):
                                   self.cfg.norm_eps, True)
         out = K.conv2d(hn, self.conv_out.w_nhwc, bias=self.conv_out.bias)
         if save:
-            rt.saved.append({"h": rt.pol(h), "st": rt.pol(st)})
+            rt.saved.append({"h": rt.pol(h), "st": rt.pol(st), "hn": hn if full else None})
         # the backward sees the policy half only
         rt.B = B
         rt.enc = rt.pol(rt.enc)
@@ -888,11 +1044,22 @@ class UNet2DConditionModel(nn.Module):
         Returns None (no gradient w.r.t. the latent input is needed on the hot path)."""
         B = dout.shape[0]
         sv = rt.saved.pop()
+        fg = rt.fg
         # conv_out input-gradient (C_out = 4): im2col of dout + GEMM with the rotated, transposed weights
         _, H, W, _ = dout.shape
         cols = K.im2col3(dout.contiguous(), self.conv_out.kp_dx)
         dhn = K.gemm(cols, self.conv_out.w_dx_col).view(B, H, W, -1)
-        dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True)
+        if fg is not None:
+            rt.dtemb = torch.zeros((B, self._temb_n), device=dout.device, dtype=torch.float32)
+            co = self.conv_out.cout
+            dy8 = torch.zeros((B * H * W, 8), device=dout.device, dtype=BF16)  # TN operands need 8 | width
+            dy8[:, :co] = dout.reshape(-1, co)
+            _conv_dw(fg, self.conv_out, dy8, K.im2col_conv(sv["hn"]))
+            dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True,
+                                  dgamma=fg.g(self.conv_norm_out.weight), dbeta=fg.g(self.conv_norm_out.bias),
+                                  accumulate=True)
+        else:
+            dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True)
         skip_grads = []
         for i in reversed(range(len(self.up_blocks))):
             blk = self.up_blocks[i]
@@ -914,7 +1081,7 @@ class UNet2DConditionModel(nn.Module):
         # the latent needs no gradient, so the backward stops there: down_blocks.0 (two 128^2 resnets + downsample),
         # down_blocks.1.resnets.0 and conv_in are never differentiated (the reference's autograd also runs them only
         # for the input gradient, which is then discarded).
-        i0, j0 = self._first_attn
+        i0, j0 = self._first_attn if fg is None else (0, -1)
         for i in reversed(range(i0, len(self.down_blocks))):
             blk = self.down_blocks[i]
             if hasattr(blk, "downsamplers"):
@@ -928,9 +1095,50 @@ class UNet2DConditionModel(nn.Module):
                 if hasattr(blk, "attentions"):
                     dh = blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}")
                 dh = blk.resnets[j].bwd(dh, rt)
+        if fg is not None:
+            dh = K.add(dh, skip_grads.pop())  # conv_in output (the first skip)
+            self._conv_in_dw(fg, dh, rt)
+            self._embed_bwd(fg, rt)
         rt.saved.clear()  # activations of the never-differentiated prefix
         rt.side.join()  # LoRA weight gradients complete before anything reads lora.grad
         return None
+
+    def _conv_in_dw(self, fg, dh, rt):
+        """conv_in (C = 4, im2col GEMM in the forward): dW = dh^T . cols on the saved patch matrix."""
+        ci = self.conv_in
+        tmp = torch.zeros((ci.cout, ci.kp), device=dh.device, dtype=torch.float32)
+        d2 = dh.reshape(-1, ci.cout)
+        K.gemm_tn(d2, rt.cols_in, tmp)
+        fg.g(ci.weight).add_(tmp[:, :9 * ci.cin].view(ci.cout, 3, 3, ci.cin).permute(0, 3, 1, 2))
+        K.colsum_acc(d2, fg.g(ci.bias).view(1, -1))
+
+    def _embed_bwd(self, fg, rt):
+        """Weight grads of the time / added-condition embeddings from the accumulated time_emb_proj output grads
+        rt.dtemb [B, sum Co]: the batched projection, silu, add_embedding and time_embedding MLPs.  The [B, 1280]
+        silu derivatives are torch element-wise ops (a few KB)."""
+        e = rt.emb
+        dt = K.cast_f32_bf16(rt.dtemb)
+        res = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        tmp = torch.zeros((self._temb_n, e["se"].shape[1]), device=dt.device, dtype=torch.float32)
+        K.gemm_tn(dt, e["se"], tmp)
+        for m in res:
+            fg.g(m.time_emb_proj.weight).add_(tmp[m._temb_off:m._temb_off + m.cout])
+            fg.g(m.time_emb_proj.bias).add_(rt.dtemb[:, m._temb_off:m._temb_off + m.cout].sum(0))
+
+        def silu_bwd(dy, x):
+            xf = x.float()
+            sg = torch.sigmoid(xf)
+            return (dy.float() * sg * (1 + xf * (1 - sg))).to(BF16)
+
+        demb = silu_bwd(K.gemm(dt, self._temb_wt), e["emb"])  # d emb (pre-silu), [B, tdim]
+        a1, a2 = self.add_embedding.linear_1, self.add_embedding.linear_2
+        _lin_dw(fg, a2, demb, e["s2"])
+        du1 = silu_bwd(K.gemm(demb, a2.wt), e["u1"])
+        _lin_dw(fg, a1, du1, e["add_in"])
+        l1, l2 = self.time_embedding.linear_1, self.time_embedding.linear_2
+        _lin_dw(fg, l2, demb, e["s1"])
+        dt1 = silu_bwd(K.gemm(demb, l2.wt), e["t1"])
+        _lin_dw(fg, l1, dt1, e["te"])
 
     @property
     def _first_attn(self):
@@ -943,9 +1151,12 @@ class UNet2DConditionModel(nn.Module):
     def forward(self, sample, timestep, encoder_hidden_states, added_cond_kwargs=None, return_dict=True, **kw):
         added = added_cond_kwargs or {}
         x = K.nchw_to_nhwc(sample)
-        need_grad = (torch.is_grad_enabled() and self.lora is not None and self._adapters_enabled)
+        # autograd trigger: the flat LoRA parameter, or (full-UNet training) a 1-element stand-in for all weights
+        trig = self.lora.param if (self.lora is not None and self._adapters_enabled) else (
+            self.full.trigger if self.full is not None else None)
+        need_grad = torch.is_grad_enabled() and trig is not None
         if need_grad:
-            out = _UNetFn.apply(x, self.lora.param, self, timestep, encoder_hidden_states, added["text_embeds"],
+            out = _UNetFn.apply(x, trig, self, timestep, encoder_hidden_states, added["text_embeds"],
                                 added["time_ids"])
         else:
             with torch.no_grad():

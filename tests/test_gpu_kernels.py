@@ -245,3 +245,47 @@ def test_gemm_skinny_n(cuda, M, N, K):
     want = acc + ref
     K_.gemm(a, w, out=acc, out_dtype=torch.float32, accumulate=True)
     assert _rel(acc, want) < 1e-5
+
+
+def test_fullgrad_helpers(cuda):
+    """pso_colsum_acc (one group / per-image groups), pso_layer_norm_dparam, pso_im2col_conv (NORMAL stride 1 / 2,
+    UP2, two concatenated sources) against torch."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(3000, 200, device=cuda, generator=g).bfloat16()
+    out = torch.randn(1, 200, device=cuda)
+    ref = out + x.float().sum(0, keepdim=True)
+    K_.colsum_acc(x, out)
+    assert _rel(out, ref) < 1e-5
+    xb = torch.randn(4 * 1024, 320, device=cuda, generator=g).bfloat16()
+    big = torch.zeros(4, 640, device=cuda)
+    K_.colsum_acc(xb, big[:, 100:420], rows_per_group=1024)
+    assert _rel(big[:, 100:420], xb.float().view(4, 1024, 320).sum(1)) < 1e-5 and big[:, :100].abs().max() == 0
+    M, C = 777, 640
+    xl = torch.randn(M, C, device=cuda, generator=g).bfloat16()
+    gm = (1 + 0.1 * torch.randn(C, device=cuda, generator=g)).bfloat16()
+    bt = (0.1 * torch.randn(C, device=cuda, generator=g)).bfloat16()
+    _, st = K_.layer_norm_fwd(xl, gm, bt, 1e-5)
+    dy = torch.randn(M, C, device=cuda, generator=g).bfloat16()
+    dg = torch.zeros(C, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    K_.layer_norm_dparam(xl, dy, st, dg, db)
+    w = gm.float().requires_grad_(True)
+    b = bt.float().requires_grad_(True)
+    y = F.layer_norm(xl.float(), (C,), w, b, 1e-5)
+    gw, gb = torch.autograd.grad(y, (w, b), dy.float())
+    assert _rel(dg, gw) < 1e-4 and _rel(db, gb) < 1e-5
+    for mode, stride, C1, C2 in [(K_.CONV_NORMAL, 1, 64, 0), (K_.CONV_NORMAL, 2, 32, 0), (K_.CONV_UP2, 1, 32, 0),
+                                 (K_.CONV_NORMAL, 1, 64, 32)]:
+        B, H, W = 2, 9, 7
+        x1 = torch.randn(B, H, W, C1, device=cuda, generator=g).bfloat16()
+        x2 = torch.randn(B, H, W, C2, device=cuda, generator=g).bfloat16() if C2 else None
+        cols = K_.im2col_conv(x1, x2, mode=mode, stride=stride)
+        xc = torch.cat([x1, x2], -1) if C2 else x1
+        xn = xc.permute(0, 3, 1, 2).float()
+        if mode == K_.CONV_UP2:
+            xn = F.interpolate(xn, scale_factor=2.0, mode="nearest")
+        u = F.unfold(xn, 3, padding=1, stride=stride)                 # [B, C*9, L] with (c, ky, kx) order
+        Ct = C1 + C2
+        u = u.view(B, Ct, 9, -1).permute(0, 3, 2, 1).reshape(-1, 9 * Ct)  # -> (pixel, tap, c)
+        assert cols.shape == u.shape and torch.equal(cols.float(), u), (mode, stride, C1, C2)
