@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="replay each epoch as one captured hipGraph (measured neutral: 31.32 vs 31.36 imgs/s eager)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--mode", default="turbo", choices=["turbo", "dmd"])
+    ap.add_argument("--full-unet", action="store_true",
+                    help="train every UNet parameter against a frozen reference UNet (BASELINE C3 / C4; use with "
+                         "--mode dmd --num-steps 4 --pairs 1 --gas 1)")
     return ap.parse_args()
 
 
@@ -58,11 +62,19 @@ def build(args, dev):
     with torch.device(dev):
         unet = UNet2DConditionModel(UNetConfig.sdxl(h))
     unet.init_weights(0)  # same frozen weights on every rank
-    unet.add_adapter(SimpleNamespace(r=args.rank, lora_alpha=args.rank))
-    unet.lora.init_gaussian(seed=0, b_std=1e-3)  # non-zero B so policy != reference
+    ref_unet = None
+    if args.full_unet:  # C3 / C4: every parameter trained, the reference is a frozen copy of the initial UNet
+        with torch.device(dev):
+            ref_unet = UNet2DConditionModel(UNetConfig.sdxl(h))
+        ref_unet.init_weights(0)
+        ref_unet.prepare()
+        unet.enable_full_grads()
+    else:
+        unet.add_adapter(SimpleNamespace(r=args.rank, lora_alpha=args.rank))
+        unet.lora.init_gaussian(seed=0, b_std=1e-3)  # non-zero B so policy != reference
     unet.prepare()
-    tr = PSOTrainer(unet, mode="turbo", num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
-                    train_batch_size=args.pairs, num_reward=1)
+    tr = PSOTrainer(unet, mode=args.mode, num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
+                    train_batch_size=args.pairs, num_reward=1, ref_unet=ref_unet)
     g = torch.Generator(device=dev).manual_seed(1000 + int(os.environ.get("RANK", "0")))
     Bp = args.pairs * args.gas  # pairs sampled per epoch per GPU
     enc = torch.randn(Bp, 77, 2048, device=dev, generator=g).bfloat16()
@@ -185,14 +197,18 @@ def main():
         "value": round(value, 3), "unit": "imgs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16", "data": "synthetic (random-init SDXL weights, N(0,1) text embeds, own-sampler trajectories)",
-        "config": {"workload": "C2: SDXL-Turbo PSO train step, LoRA r=%d grads, %d pairs/GPU/micro-step, gas %d, "
-                               "%d-step sampler (T=%d)" % (args.rank, args.pairs, args.gas, args.num_steps,
-                                                           args.num_steps - 1),
+        "config": {"workload": ("C3/C4: SDXL-%s PSO train step, full-UNet grads vs a frozen reference UNet, %d "
+                                "pairs/GPU/micro-step, gas %d, %d-step sampler (T=%d)"
+                                % ("DMD2" if args.mode == "dmd" else "Turbo", args.pairs, args.gas, args.num_steps,
+                                   args.num_steps - 1)) if args.full_unet else
+                               ("C2: SDXL-Turbo PSO train step, LoRA r=%d grads, %d pairs/GPU/micro-step, gas %d, "
+                                "%d-step sampler (T=%d)" % (args.rank, args.pairs, args.gas, args.num_steps,
+                                                            args.num_steps - 1)),
                    "global_batch": 2 * args.pairs * world, "seq_len": (args.res // 16) ** 2, "resolution": args.res,
                    "parallelism": f"dp{world}", "launch": "hipgraph-epoch" if args.graph else "eager"},
         "loss": round(loss, 6),
     }
-    tf = SURVEY_TFLOP_PER_PAIR_MICRO.get(args.rank) if args.res == 1024 else None
+    tf = SURVEY_TFLOP_PER_PAIR_MICRO.get(args.rank) if (args.res == 1024 and not args.full_unet) else None
     if tf:
         step_tf = tf * args.pairs * args.gas * (args.num_steps - 1)
         res["step_mfma_frac"] = round(step_tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)

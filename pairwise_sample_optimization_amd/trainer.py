@@ -70,25 +70,34 @@ def allreduce_grads(flat, process_group=None):
     return 1.0 / world
 
 
+def trainable(unet):
+    """(master, grad, refresh) of what the step trains: the flat LoRA bucket (the reference's recipe), or every UNet
+    parameter when unet.enable_full_grads() was called (BASELINE C3 / C4, build-only)."""
+    if getattr(unet, "full", None) is not None:
+        return unet.full.master, unet.full.grad, unet.refresh_full
+    st = unet.lora
+    return st.master, st.grad, st.refresh
+
+
 def lora_optimizer_step(tr):
     """accelerator.backward's sync step + clip_grad_norm_ + optimizer.step + zero_grad (T:857-861, DB:1953-1964) on
     the flat LoRA bucket of tr.unet: RCCL all-reduce -> global-norm clip coefficient -> fused AdamW (clip and 1/world
     folded into the gradient read) -> zero -> refresh the bf16 working copies.  tr carries exp_avg, exp_avg_sq,
     opt_step, clip_buf, lr, betas, adam_eps, wd, max_grad_norm, pg."""
-    st = tr.unet.lora
-    scale = allreduce_grads(st.grad, tr.pg)
-    K.grad_clip_coef(st.grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
+    master, grad, refresh = trainable(tr.unet)
+    scale = allreduce_grads(grad, tr.pg)
+    K.grad_clip_coef(grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
     tr.opt_step += 1
-    K.adamw_step(st.master, st.grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
+    K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
                  grad_scale=scale, clip=tr.clip_buf)
-    K.zero_(st.grad)
-    st.refresh()
+    K.zero_(grad)
+    refresh()
 
 
 class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
-                 train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16):
+                 train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None):
         self.unet = unet
         self.mode = MODE_TURBO if mode == "turbo" else MODE_DMD
         self.num_steps = num_steps
@@ -102,12 +111,17 @@ class PSOTrainer:
         self.m = num_reward
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
-        st = unet.lora
-        self.exp_avg = torch.zeros_like(st.master)
-        self.exp_avg_sq = torch.zeros_like(st.master)
+        master, _, _ = trainable(unet)
+        self.exp_avg = torch.zeros_like(master)
+        self.exp_avg_sq = torch.zeros_like(master)
         self.opt_step = 0
         self.n_micro = 0
-        self.clip_buf = torch.zeros(2, device=st.master.device, dtype=torch.float32)
+        self.clip_buf = torch.zeros(2, device=master.device, dtype=torch.float32)
+        # full-UNet training (C3 / C4): the reference model is a frozen copy of the initial UNet (App. A #4), run as
+        # its own forward instead of the adapter-free half of a paired pass
+        self.ref_unet = ref_unet
+        if getattr(unet, "full", None) is not None and ref_unet is None:
+            raise ValueError("full-UNet training needs ref_unet (a frozen copy of the initial weights)")
         self.loss_hist = []
         self.max_pass_images = max_pass_images  # images per batched UNet pass (HBM budget: ~5 GB saved each @1024^2)
         self.auto_step = True  # run the optimizer every gas*T micro-steps (tests may inspect raw grads)
@@ -119,14 +133,14 @@ class PSOTrainer:
             self.sched = LCMScheduler()
             ts, self.step_ratio = dmd_distill_timesteps(num_steps)
             self.timesteps = ts.float()
-        dev = st.master.device
+        dev = master.device
         self.timesteps_dev = self.timesteps.to(dev)
         # per-transition step coefficients [T, 8], host-computed once, device resident
         self.coef_dev = torch.stack([self.coef_for_step(j, 1)[0] for j in range(self.T)], 0).to(dev) \
             if self.T > 0 else torch.zeros(0, 8, device=dev)
 
     @classmethod
-    def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None):
+    def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None, ref_unet=None):
         """Build from a reference run config (`config_sdxl_{turbo,dmd}_dpo.get_config()`): sample.num_steps,
         train.{beta, eps, learning_rate, adam_*, max_grad_norm, gradient_accumulation_steps, batch_size}.
         Turbo enforces `distilled_train_steps == num_steps - 1` like T:221."""
@@ -137,7 +151,7 @@ class PSOTrainer:
                    lr=tr.learning_rate, betas=(tr.adam_beta1, tr.adam_beta2), weight_decay=tr.adam_weight_decay,
                    adam_eps=tr.adam_epsilon, max_grad_norm=tr.max_grad_norm,
                    gradient_accumulation_steps=tr.gradient_accumulation_steps, train_batch_size=tr.batch_size,
-                   num_reward=num_reward, process_group=process_group)
+                   num_reward=num_reward, process_group=process_group, ref_unet=ref_unet)
 
     # ------------------------------------------------------------------------------------------------------------
     # coefficients of transition j (host float32 scalars, the reference's operation order)
@@ -268,11 +282,16 @@ class PSOTrainer:
             raise ValueError("a batched pass must not cross an optimizer step")
         P = self.P * count
         u = self.unet
-        u.enable_adapters()
-        # policy (LoRA on, T:775-787) and reference (adapters disabled, T:790-805) eps of the same inputs in ONE pass
-        eps_both, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True, paired_ref=True)
-        n = mb.unet_in.shape[0]
-        eps_pol, eps_ref = eps_both[:n], eps_both[n:]
+        if self.ref_unet is not None:  # full-UNet training: policy pass + the frozen reference UNet's pass
+            eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
+            with torch.no_grad():
+                eps_ref, _ = self.ref_unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
+        else:
+            u.enable_adapters()
+            # policy (LoRA on, T:775-787) and reference (adapters disabled, T:790-805) eps of the same inputs in ONE pass
+            eps_both, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True, paired_ref=True)
+            n = mb.unet_in.shape[0]
+            eps_pol, eps_ref = eps_both[:n], eps_both[n:]
         idx = None
         if self.mode == MODE_TURBO and self.m > 1:  # sample_compare draws a reward column per pair (T:405)
             idx = torch.randint(0, self.m, (P,), device=mb.x.device, generator=generator)
@@ -315,8 +334,8 @@ class PSOTrainer:
             self._graph = None
             self._gsb = SimpleNamespace(n_micro=sb.n_micro, P=sb.P,
                                         **{k: getattr(sb, k).clone() for k in self._SB_TENSORS})
-            st = self.unet.lora
-            saved = st.grad.clone()
+            _, st_grad, _ = trainable(self.unet)
+            saved = st_grad.clone()
             self.auto_step = False
             n0, h0 = self.n_micro, len(self.loss_hist)
             try:
@@ -331,7 +350,7 @@ class PSOTrainer:
                 self.auto_step = True
                 self.n_micro = n0
                 del self.loss_hist[h0:]
-                st.grad.copy_(saved)
+                st_grad.copy_(saved)
             self._graph, self._graph_key = g, key
         for k in self._SB_TENSORS:
             getattr(self._gsb, k).copy_(getattr(sb, k))
