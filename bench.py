@@ -170,6 +170,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(rank)
+    if os.environ.get("PSO_BENCH_GEMM_VARIANT"):  # A/B knob of the GEMM dispatch (tools/_ab.sh)
+        from pairwise_sample_optimization_amd import kernels as K
+        K.lib().pso_gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
     t_build = time.time()
     unet, tr, buf, g = build(args, dev)
     log(f"[bench] built + sampled in {time.time() - t_build:.1f}s; warmup {args.warmup}")

@@ -46,6 +46,7 @@ struct GemmArgs {
   const bf16_t* resid; long ldr;
   void* out; long ldo; int out_dtype; int accumulate;
   int vec_ok;  // 4-wide epilogue vectors are aligned
+  int stage_epi;  // bf16 EPI_NONE epilogue staged through LDS: 16-B coalesced residual loads / output stores
   int group_m;  // tile rows per raster group (>= 1)
   // GEGLU epilogues (diffusers GEGLU: [h | gate] = x W^T + b, out = h * gelu(gate)), weight rows interleaved per 64
   // columns as [h 32 | gate 32]:  EPI_GEGLU writes out = h*gelu(gate) (N/2 columns) and, if out2, the interleaved
@@ -521,6 +522,81 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     }
     return;
   }
+  if constexpr (EPI == EPI_NONE && !PIPE && BM * (BN + 8) * 2 <= STAGES * (BM + BN) * BK * 2) {
+    if (g.stage_epi && epi_fast && g.out_dtype == PSO_BF16 && !g.accumulate && nt > 0) {
+      // Staged epilogue: y = bf16(acc * alpha + bias [+ rowbias]) goes to LDS in the MFMA layout, then the workgroup
+      // walks the tile in 16-B chunks: residual loaded and output stored as whole 16-B vectors (half the store
+      // instructions of the 8-B per-lane layout).  The residual is added to the bf16-rounded projection, as the
+      // unfused Linear + add does.
+      constexpr int TP = BN + 8;
+      constexpr int NT = 64 * WM * WN;
+      constexpr int CC = BN / 8;
+      constexpr int ITERS = (BM * CC + NT - 1) / NT;
+      const bool rowb = g.rowbias != nullptr;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
+        ebias[j] = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
+      }
+      if (rowb) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int m = min(m0 + wm * (BM / WM) + i * 16 + fr, g.M - 1);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            eadd[i][j] = *reinterpret_cast<const uint2*>(g.rowbias + (long)(m / g.rows_per_group) * g.ld_rowbias + n0 +
+                                                         wn * (BN / WN) + j * 16 + fk * 4);
+        }
+      }
+      __syncthreads();  // every wave is done with the operand ring
+      bf16_t* tl = lds_base;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int ml = wm * (BM / WM) + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int nl = wn * (BN / WN) + j * 16 + fk * 4;
+          float v[4] = {acc[i][j][0] * g.alpha + bf2f(ebias[j].x & 0xffff), acc[i][j][1] * g.alpha + bf2f(ebias[j].x >> 16),
+                        acc[i][j][2] * g.alpha + bf2f(ebias[j].y & 0xffff), acc[i][j][3] * g.alpha + bf2f(ebias[j].y >> 16)};
+          if (rowb) {
+            v[0] += bf2f(eadd[i][j].x & 0xffff); v[1] += bf2f(eadd[i][j].x >> 16);
+            v[2] += bf2f(eadd[i][j].y & 0xffff); v[3] += bf2f(eadd[i][j].y >> 16);
+          }
+          *reinterpret_cast<uint2*>(tl + ml * TP + nl) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+      }
+      // residual chunks: every load in flight at once (the accumulators are dead now)
+      uint4 rr[ITERS];
+      if (g.resid) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+          const int q = threadIdx.x + it * NT;
+          const int ml = q / CC, cl = (q - (q / CC) * CC) * 8;
+          const int m = min(m0 + ml, g.M - 1);
+          if (q < BM * CC) rr[it] = *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + cl);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int q = threadIdx.x + it * NT;
+        const int ml = q / CC, cl = (q - (q / CC) * CC) * 8;
+        const int m = m0 + ml;
+        if (q >= BM * CC || m >= g.M) continue;
+        uint4 y = *reinterpret_cast<const uint4*>(tl + ml * TP + cl);
+        if (g.resid) {
+          const uint32_t yw[4] = {y.x, y.y, y.z, y.w}, rw[4] = {rr[it].x, rr[it].y, rr[it].z, rr[it].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = pack2bf(bf2f(yw[e] & 0xffff) + bf2f(rw[e] & 0xffff), bf2f(yw[e] >> 16) + bf2f(rw[e] >> 16));
+          y = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + cl) = y;
+      }
+      return;
+    }
+  }
   if (!PIPE && epi_fast && nt > 0) {
     epi_prefetch();  // every epilogue load in flight at once, then the arithmetic and the stores
     const bool has_add = g.resid || g.rowbias;
@@ -669,12 +745,18 @@ static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
+  const int gv_raw = g_gemm_variant;
+  const int gv = gv_raw == 41 ? 0 : gv_raw;  // 41 = automatic dispatch with the per-lane epilogue
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
     pso_set_error("pso_gemm: tail_group_n must be a multiple of 64");
     return PSO_ERR_ARG;
   }
+  // staged 16-B epilogue for bf16 outputs with 16-B aligned rows (5-10 % on the K = 640 / 1280 projections with
+  // bias + residual, tools/epi_bench.py); variant 41 keeps the per-lane 8-B epilogue (A/B knob)
+  g.stage_epi = gv_raw != 41 && g.out_dtype == PSO_BF16 && al16(g.out) && (g.ldo % 8) == 0 &&
+                (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0));
   g.vec_ok = (g.ldo % 4) == 0 && (g.out_dtype == PSO_F32 ? al16(g.out) : al8(g.out)) &&
              (!g.resid || ((g.ldr % 4) == 0 && al8(g.resid))) && (!g.bias || al8(g.bias)) &&
              (!g.rowbias || (al8(g.rowbias) && (g.ld_rowbias % 4) == 0));
@@ -682,7 +764,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const bool bn256_ok = g.tail_group_n == 0 || (g.tail_group_n % 256) == 0;
   const long Ktot = (long)g.K1 + (g.a2 ? g.K2 : 0);
   // Skinny N (the LoRA rank-r products): one 16-row x all-N tile per 4-wave block, K split over the waves.
-  if (g_gemm_variant == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
+  if (gv == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
       (g.N % 4) == 0 && g.vec_ok && g.M >= 256)
     return pso_gemm_skinny_nt(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.alpha, g.out, g.ldo,
                               g.out_dtype == PSO_F32, g.accumulate, 1, st);
@@ -702,26 +784,26 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
                    g.alpha == 1.f && (g.N % 256) == 0 && (g.K1 % 128) == 0 && g.vec_ok && al16(g.a1) && al16(g.b1) &&
                    (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 && (long)g.M * g.lda1 < (1L << 30) &&
                    (long)g.N * g.ldb1 < (1L << 30);
-  if (g_gemm_variant == 30 && ok8)
+  if (gv == 30 && ok8)
     return pso_gemm8p(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.bias, g.out, g.ldo, g.group_m, st);
-  if (g_gemm_variant == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
-  if (g_gemm_variant == 2 && !bn64_only) return launch<128, 128, 2, 2, 3>(g, st);
-  if (g_gemm_variant == 3 && !bn64_only) return launch<128, 128>(g, st);
-  if (g_gemm_variant == 6 && !bn64_only) return launch<64, 128>(g, st);
-  if (g_gemm_variant == 7 && bn256_ok) return launch<128, 256, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 8 && !bn64_only) return launch<128, 128, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 10 && bn256_ok) return launch<256, 256, 2, 4, 2, true>(g, st);
-  if (g_gemm_variant == 11 && !bn64_only) return launch<128, 128, 2, 4, 2, true>(g, st);
+  if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
+  if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
+  if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
+  if (gv == 2 && !bn64_only) return launch<128, 128, 2, 2, 3>(g, st);
+  if (gv == 3 && !bn64_only) return launch<128, 128>(g, st);
+  if (gv == 6 && !bn64_only) return launch<64, 128>(g, st);
+  if (gv == 7 && bn256_ok) return launch<128, 256, 2, 4, 2>(g, st);
+  if (gv == 8 && !bn64_only) return launch<128, 128, 2, 4, 2>(g, st);
+  if (gv == 10 && bn256_ok) return launch<256, 256, 2, 4, 2, true>(g, st);
+  if (gv == 11 && !bn64_only) return launch<128, 128, 2, 4, 2, true>(g, st);
   const bool n160 = (g.N % 160) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
   const bool n320 = (g.N % 320) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
-  if (g_gemm_variant == 12 && n160) return launch<128, 160, 2, 2, 2>(g, st);
-  if (g_gemm_variant == 14 && n160) return launch<256, 160, 2, 2, 2>(g, st);
-  if (g_gemm_variant == 16 && n160) return launch<256, 160, 2, 2, 2, true>(g, st);
-  if (g_gemm_variant == 17 && n320) return launch<128, 320, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 18 && n320) return launch<256, 320, 2, 4, 2>(g, st);
-  if (g_gemm_variant == 19 && n160) return launch<128, 160, 2, 2, 2, true>(g, st);
+  if (gv == 12 && n160) return launch<128, 160, 2, 2, 2>(g, st);
+  if (gv == 14 && n160) return launch<256, 160, 2, 2, 2>(g, st);
+  if (gv == 16 && n160) return launch<256, 160, 2, 2, 2, true>(g, st);
+  if (gv == 17 && n320) return launch<128, 320, 2, 4, 2>(g, st);
+  if (gv == 18 && n320) return launch<256, 320, 2, 4, 2>(g, st);
+  if (gv == 19 && n160) return launch<128, 160, 2, 2, 2, true>(g, st);
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).

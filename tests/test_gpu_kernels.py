@@ -160,7 +160,7 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
 @pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
                                         (8192, 640, 320, 0), (1000, 700, 136, 0)])
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
@@ -213,7 +213,7 @@ def test_gemm_8phase(cuda, M, N, K):
         K_.lib().pso_gemm_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
 def test_conv_every_variant_large(cuda, variant):
     from pairwise_sample_optimization_amd import kernels as K_
     K_.lib().pso_gemm_set_variant(variant)
