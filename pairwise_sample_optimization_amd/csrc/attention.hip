@@ -131,9 +131,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // (global_load_lds_dwordx4, 2 K + 2 V pieces of 8 rows x 128 B per wave per tile) through a 3-stage ring, two tiles in
 // flight behind a counted vmcnt and ONE s_barrier per tile.  The LDS swizzles are applied on the source side (lane i of
 // a piece lands at byte 16*i): K row-image chunk p ^ (row & 7), V transposed-read chunk p ^ 2*((row >> 1) & 3).
-// Softmax: raw-score running max (exp2(s*c - m*c) = one FMA + one exp per score), per-lane partial row sums reduced
-// once at the end, the O/l rescale skipped when no row max moved (wave-uniform), key masking on the last tile only.
-template <int QI>
+// Softmax: raw-score running max (exp2(s*c - m*c) = one FMA + one exp per score), row sums accumulated by one extra
+// MFMA per PV step against an all-ones operand (no per-score VALU add, no cross-lane reduction), the O/l rescale
+// skipped when no row max moved (wave-uniform), key masking on the last tile only.
+template <int QI, bool MSUM = true>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, int nqb) {
   constexpr int STG = 3;
   constexpr int PIECES = 4;  // glds per wave per tile
@@ -180,11 +181,15 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
   if (nkt > 1) issue(1, 1);
 
   f32x4 o[QI][4];
-  float m_run[QI], l_run[QI];
+  // row sums on the matrix cores: lsum[qi] += 1^T . P^T (an all-ones A operand), so every lane gets the full row sum
+  // of its query without a VALU add per score or a cross-lane reduction; it sums the bf16 P the PV product uses
+  f32x4 lsum[QI];
+  float m_run[QI];
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
 #pragma unroll
   for (int qi = 0; qi < QI; ++qi) {
     m_run[qi] = -INFINITY;
-    l_run[qi] = 0.f;
+    lsum[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[qi][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
       const float m_new = fmaxf(m_run[qi], mx);
       if (__any(m_new > m_run[qi])) {
         const float alpha = fast_exp2((m_run[qi] - m_new) * c2);  // first tile: exp2(-inf) = 0
-        l_run[qi] *= alpha;
+        lsum[qi] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[qi][dt] *= alpha;
         m_run[qi] = m_new;
@@ -244,18 +249,20 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
       for (int kj = 0; kj < 4; ++kj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(fmaf(s[qi][kj][r], c2, -mc));
-          s[qi][kj][r] = p;
-          sum += p;
+          s[qi][kj][r] = fast_exp2(fmaf(s[qi][kj][r], c2, -mc));
+          if (!MSUM) sum += s[qi][kj][r];
         }
-      l_run[qi] += sum;  // this lane's keys only; the 4 lanes of a row are summed in the epilogue
+      if (!MSUM) lsum[qi][0] += sum;  // VALU form (A/B knob): this lane's keys; the 4 lanes summed at the end
     }
     // ---- O^T += V^T . P^T ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 pf[QI];
 #pragma unroll
-      for (int qi = 0; qi < QI; ++qi) pf[qi] = pack_p(s[qi][2 * ks], s[qi][2 * ks + 1]);
+      for (int qi = 0; qi < QI; ++qi) {
+        pf[qi] = pack_p(s[qi][2 * ks], s[qi][2 * ks + 1]);
+        if (MSUM) lsum[qi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qi], lsum[qi], 0, 0, 0);
+      }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const s16x4 v0 = tr_read(v_img, (2 * ks) * 16 + 4 * g, dt * 16, lane);
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
   bf16_t* O = a.o + b * a.so_b + h * ATT_D;
 #pragma unroll
   for (int qi = 0; qi < QI; ++qi) {
-    const float l = rowsum4(l_run[qi]);
+    const float l = MSUM ? lsum[qi][0] : rowsum4(lsum[qi][0]);  // MSUM: every element holds the query's row sum
     const int qr = q0 + qi * 16 + c;
     if (qr >= a.Sq) continue;
     const float inv = 1.f / l;
@@ -654,6 +661,7 @@ static int cross_qsplit(int B, int H, int Sq, int Sk) {
 }
 
 static int g_attn_fwd_variant = 0;
+static bool g_attn_vsum = false;
 static int g_attn_bwd_variant = 0;  // benchmark knob: 0 auto, 2 / 4 = keys per wave / 16  // benchmark knob: 0 auto, 2 / 4 = queries per wave / 16
 
 static bool a16(const void* p, long ld) { return (((uintptr_t)p) & 15) == 0 && (ld % 8) == 0; }
@@ -662,7 +670,8 @@ extern "C" {
 
 void pso_attention_set_variant(int v) {
   g_attn_fwd_variant = v % 10;
-  g_attn_bwd_variant = v / 10;
+  g_attn_bwd_variant = (v / 10) % 10;
+  g_attn_vsum = v >= 100;  // 100+: row sums on the VALU (A/B knob)
 }
 
 int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
@@ -681,8 +690,14 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // workgroups, else 128 (4 x 32): fewer K/V LDS bytes per MFMA vs. a fuller grid
   const int nq4 = cdiv(Sq, 256), nq2 = cdiv(Sq, 128);
   const bool big = g_attn_fwd_variant == 4 || (g_attn_fwd_variant == 0 && (long)nq4 * H * B >= 1024);
-  if (big) attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
-  else attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
+  if (g_attn_vsum) {
+    if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
+    else attn_fwd_kernel<2, false><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
+  } else if (big) {
+    attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
+  } else {
+    attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
+  }
   return pso_check_launch("pso_attention_fwd");
 }
 
