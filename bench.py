@@ -173,6 +173,9 @@ def main():
     if os.environ.get("PSO_BENCH_GEMM_VARIANT"):  # A/B knob of the GEMM dispatch (tools/_ab.sh)
         from pairwise_sample_optimization_amd import kernels as K
         K.lib().pso_gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
+    if os.environ.get("PSO_BENCH_ATTN_VARIANT"):  # A/B knob of the attention kernels
+        from pairwise_sample_optimization_amd import kernels as K
+        K.lib().pso_attention_set_variant(int(os.environ["PSO_BENCH_ATTN_VARIANT"]))
     t_build = time.time()
     unet, tr, buf, g = build(args, dev)
     log(f"[bench] built + sampled in {time.time() - t_build:.1f}s; warmup {args.warmup}")

@@ -47,6 +47,10 @@ def run(dev):
         ref = a.float() @ w.float().t()
         err = ((K.gemm(a, w).float() - ref).norm() / ref.norm()).item()
         rows.append((name, f"{M}x{N}x{Kd} e={err:.1e}", ms, 2 * M * N * Kd / ms / 1e9))
+        if os.environ.get("GEMM_LIB"):  # hipBLASLt (torch.mm) on the same operands, for the headroom column only
+            wt = w.t()
+            ms = t_ms(lambda: torch.mm(a, wt))
+            rows.append(("  hipBLASLt " + name, f"{M}x{N}x{Kd}", ms, 2 * M * N * Kd / ms / 1e9))
     for (M, F, Kd, name) in [(2 * L2, 5120, 1280, "L2x2 geglu"), (2 * L1, 2560, 640, "L1x2 geglu")]:
         a = torch.randn(M, Kd, device=dev).bfloat16()
         w = (torch.randn(2 * F, Kd, device=dev) / Kd ** 0.5).bfloat16()
