@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpso_amd.so")
+LIB_PATH = os.environ.get("PSO_LIB_PATH") or os.path.join(_HERE, "libpso_amd.so")  # override: same-box A/B only
 
 PSO_F32 = 0
 PSO_BF16 = 1

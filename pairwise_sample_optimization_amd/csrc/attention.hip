@@ -294,36 +294,6 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
 }
 
 // ================================================================================================================
-// backward pre-pass: delta[b][h][q] = sum_d dO * O
-// ================================================================================================================
-__global__ void attn_delta_kernel(AttnArgs a, int B) {
-  const long idx = blockIdx.x * (long)(blockDim.x / 64) + (threadIdx.x >> 6);  // one wave per (b, q), all heads
-  const int lane = threadIdx.x & 63;
-  if (idx >= (long)B * a.Sq) return;
-  const int b = (int)(idx / a.Sq), q = (int)(idx - (long)b * a.Sq);
-  const bf16_t* O = a.o + b * a.so_b + (long)q * a.ldo;
-  const bf16_t* D = a.dO + b * a.sdo_b + (long)q * a.lddo;
-  // each head = 64 d = 8 chunks; lane handles chunk (lane & 7) of heads (lane >> 3) + 8k
-  for (int h0 = 0; h0 < a.H; h0 += 8) {
-    const int h = h0 + (lane >> 3);
-    float s = 0.f;
-    if (h < a.H) {
-      const int off = h * ATT_D + (lane & 7) * 8;
-      const uint4 ov = *reinterpret_cast<const uint4*>(O + off);
-      const uint4 dv = *reinterpret_cast<const uint4*>(D + off);
-      const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        s += bf2f(ow[j] & 0xffff) * bf2f(dw[j] & 0xffff) + bf2f(ow[j] >> 16) * bf2f(dw[j] >> 16);
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    if (h < a.H && (lane & 7) == 0) a.delta[((long)b * a.H + h) * a.Sq + q] = s;
-  }
-}
-
-// ================================================================================================================
 // backward dK/dV: one workgroup = 4 waves x (16*KJ) keys of one (b, h) (keys on the MFMA lane axis); query tiles of
 // 64 stream through a STG-stage LDS ring filled directly from global memory: per tile the Q row image, the Q
 // transposed-read image, the dO row image, the dO transposed-read image (8 pieces of 8 rows x 128 B each, 8 per wave)
@@ -507,7 +477,8 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 }
 
 // ================================================================================================================
-// backward dQ: forward structure (128 queries per workgroup, S^T = K.Q^T lane-local per query), K/V tiles through LDS
+// backward dQ: forward structure (128 queries per workgroup, S^T = K.Q^T lane-local per query), K/V tiles through LDS;
+// also forms delta[b][h][q] = sum_d dO * O for its queries (stored for the dK/dV kernel launched after it)
 //   dP^T = V . dO^T ; dS^T = P^T * (dP^T - delta) ; dQ^T[d][q] += K^T . dS^T  (K^T via transposed reads)
 // ================================================================================================================
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a) {
@@ -529,21 +500,32 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
 
   bf16x8 qf[2][2], of[2][2];
   float lq[2], dl[2];
+  const bf16_t* O = a.o + b * a.so_b + h * ATT_D;
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     const int qr = q0 + qi * 16 + c;
+    float part = 0.f;  // delta = sum_d dO * O of this query: lanes c, c+16, c+32, c+48 hold its 64 d (2 x 8 each)
 #pragma unroll
     for (int ds = 0; ds < 2; ++ds) {
-      uint4 v = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0);
+      uint4 v = make_uint4(0, 0, 0, 0), w = make_uint4(0, 0, 0, 0), u = make_uint4(0, 0, 0, 0);
       if (qr < a.Sq) {
         v = *reinterpret_cast<const uint4*>(Q + (long)qr * a.ldq + ds * 32 + 8 * g);
         w = *reinterpret_cast<const uint4*>(DO + (long)qr * a.lddo + ds * 32 + 8 * g);
+        u = *reinterpret_cast<const uint4*>(O + (long)qr * a.ldo + ds * 32 + 8 * g);
       }
       qf[qi][ds] = __builtin_bit_cast(bf16x8, v);
       of[qi][ds] = __builtin_bit_cast(bf16x8, w);
+      const uint32_t ow[4] = {u.x, u.y, u.z, u.w}, dw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        part += bf2f(ow[j] & 0xffff) * bf2f(dw[j] & 0xffff) + bf2f(ow[j] >> 16) * bf2f(dw[j] >> 16);
     }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    dl[qi] = part;
     lq[qi] = qr < a.Sq ? a.lse[((long)b * a.H + h) * a.Sq + qr] * ln2inv : INFINITY;
-    dl[qi] = qr < a.Sq ? a.delta[((long)b * a.H + h) * a.Sq + qr] : 0.f;
+    // published for the dK/dV kernel, which runs after this one on the stream
+    if (qr < a.Sq && g == 0) a.delta[((long)b * a.H + h) * a.Sq + qr] = part;
   }
   f32x4 dq[2][4];
 #pragma unroll
@@ -739,7 +721,9 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   }
   a.q_split = qsplit;
   a.nbatch = B;
-  attn_delta_kernel<<<cdiv((long)B * Sq, 4), 256, 0, st>>>(a, B);
+  // dQ first: it forms delta = rowsum(dO * O) for its own queries and stores it for the dK/dV sweep (no separate
+  // delta pre-pass launch)
+  attn_bwd_dq_kernel<<<dim3(cdiv(Sq, 128), H, B), ATT_THREADS, 0, st>>>(a);
   // keys per wave: 32 (2 x 16, 128 keys per workgroup, 2 workgroups per CU); 64 on request (benchmark knob)
   const int nkb4 = cdiv(Sk, 256);
   const bool kj4 = g_attn_bwd_variant == 4;  // measured slower on every UNet shape (1 wave/SIMD, AGPR spills)
@@ -756,7 +740,6 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
     const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
     attn_bwd_dkv_kernel<2, 2><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
   }
-  attn_bwd_dq_kernel<<<dim3(cdiv(Sq, 128), H, B), ATT_THREADS, 0, st>>>(a);
   if (qsplit > 1) {
     // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)
     const long rows = (long)B * Sk;

@@ -1029,6 +1029,11 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   if (g_gemm_variant == 32 && (K % 128) == 0 && (long)M * lda < (1L << 30) && (long)N * ldw < (1L << 30))
     return pso_gemm8p_geglu(M, N, K, a, lda, w, ldw, bias, out, ldo, out_pre, ld_pre, g.tail_m, g.group_m,
                             (hipStream_t)stream);
+  // tile A/B knobs (64-column wave tiles are what the interleaved epilogue needs)
+  if (g_gemm_variant == 33) return launch<128, 128, 2, 2, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
+  if (g_gemm_variant == 34) return launch<128, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
+  if (g_gemm_variant == 35) return launch<256, 128, 4, 2, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
+  if (g_gemm_variant == 36) return launch<128, 128, 2, 2, 3, false, EPI_GEGLU>(g, (hipStream_t)stream);
   return launch<256, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
 }
 
