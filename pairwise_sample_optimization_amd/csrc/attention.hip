@@ -616,9 +616,14 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
   }
 }
 
-// dst[r][c] = bf16( sum_s src[s][r][c] ) : the query-split partials of the cross-attention dK / dV
-__global__ void reduce_splits_kernel(long rows, int cols, int nsplit, const float* __restrict__ src, long split_stride,
-                                     bf16_t* __restrict__ dst, long ldd) {
+// dst[r][c] = bf16( sum_s src[s][r][c] ) : the query-split partials of the cross-attention dK (blockIdx.y = 0) and
+// dV (blockIdx.y = 1) in one launch
+__global__ void reduce_splits_kernel(long rows, int cols, int nsplit, const float* __restrict__ src_k,
+                                     const float* __restrict__ src_v, long split_stride, bf16_t* __restrict__ dst_k,
+                                     long ldd_k, bf16_t* __restrict__ dst_v, long ldd_v) {
+  const float* __restrict__ src = blockIdx.y ? src_v : src_k;
+  bf16_t* __restrict__ dst = blockIdx.y ? dst_v : dst_k;
+  const long ldd = blockIdx.y ? ldd_v : ldd_k;
   const int c4 = cols / 4;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * c4; i += (long)gridDim.x * blockDim.x) {
     const long r = i / c4;
@@ -745,8 +750,8 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
     const long rows = (long)B * Sk;
     const int cols = H * ATT_D;
     const int nb = cdiv(rows * cols / 4, 256) > 2048 ? 2048 : cdiv(rows * cols / 4, 256);
-    reduce_splits_kernel<<<nb, 256, 0, st>>>(rows, cols, qsplit, a.dk_acc, part, (bf16_t*)dk, lddk);
-    reduce_splits_kernel<<<nb, 256, 0, st>>>(rows, cols, qsplit, a.dv_acc, part, (bf16_t*)dv, lddv);
+    reduce_splits_kernel<<<dim3(nb, 2), 256, 0, st>>>(rows, cols, qsplit, a.dk_acc, a.dv_acc, part, (bf16_t*)dk, lddk,
+                                                      (bf16_t*)dv, lddv);
   }
   return pso_check_launch("pso_attention_bwd");
 }

@@ -259,6 +259,14 @@ class LoraState:
                       (ns.sB_o2, ns.sBt_o2)]
             self.blk[path] = ns
         self._transposes = K.BatchedTranspose(pairs, device) if device.type == "cuda" else None
+        # per width C: the k/v adapters of its blocks stacked in block order, A [n*2r, Dc] and sB [n*2C, r], for the
+        # width-batched text K/V projection (UNet2DConditionModel.kv_text); rebuilt by refresh()
+        by_c = {}
+        for path, C, Dc in blocks:
+            by_c.setdefault(C, []).append(self.blk[path])
+        self.kv_stacks = {C: (torch.empty(len(bl) * 2 * r, bl[0].A_kv2.shape[1], device=device, dtype=BF16),
+                              torch.empty(len(bl) * 2 * C, r, device=device, dtype=BF16), bl)
+                          for C, bl in by_c.items()}
         self._b_views = [self.seg(self.work, p, k) for p, _, _ in blocks for k in self.layout[p] if ".B_" in k]
 
     def seg(self, t, path, key):
@@ -313,6 +321,9 @@ class LoraState:
             for Bw in self._b_views:
                 K.axpby(self.scale, Bw, out=Bw)
         self._transposes()
+        for A, sB, bl in self.kv_stacks.values():
+            torch.cat([L.A_kv2 for L in bl], 0, out=A)
+            torch.cat([L.sB_kv2 for L in bl], 0, out=sB)
 
     def grad_seg(self, path, key):
         return self.seg(self.grad, path, key)
@@ -416,13 +427,13 @@ class BasicTransformerBlock(nn.Module):
         if lo:
             u_q2 = K.gemm(pol(n2), L.A_q2)
             q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
-            u_kv2 = K.gemm(pol(enc), L.A_kv2)                               # [Bp*77, 2r]
-            kv2 = K.gemm(enc, a2m.w_kv, a2=u_kv2, w2=L.sB_kv2, tail_group_n=C,
-                         tail_rows=enc.shape[0] // 2 if rt.paired else 0)
         else:
             q2 = K.gemm(n2, a2m.to_q.weight)
-            kv2 = K.gemm(enc, a2m.w_kv)
-        kv3 = kv2.view(B, Se, 2 * C)
+        # K/V of the text tokens: this block's columns of the width-batched projection (UNet2DConditionModel.kv_text)
+        kv_all, u_all = rt.kv_text(C)
+        j = self._kv_slot
+        kv3 = kv_all.view(B, Se, -1)[..., j * 2 * C:(j + 1) * 2 * C]        # [B, 77, 2C] view
+        u_kv2 = u_all[:, j * 2 * r:(j + 1) * 2 * r] if lo else None          # [Bp*77, 2r] view
         a2, lse2 = K.attention_fwd(q2.view(B, S, C), kv3[..., :C], kv3[..., C:], a2m.heads)
         a2 = a2.view(M, C)
         o2 = a2m.to_out[0]
@@ -439,7 +450,7 @@ class BasicTransformerBlock(nn.Module):
         h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
         if rt.save:  # the backward runs on the policy images only
             sv = dict(x=pol(x), st1=pol(st1), n1=pol(n1), qkv=pol(qkv), a1=pol(a1), lse1=pol(lse1), h1=pol(h1),
-                      st2=pol(st2), n2=pol(n2), q2=pol(q2), kv2=pol(kv2), a2=pol(a2), lse2=pol(lse2), h2=pol(h2),
+                      st2=pol(st2), n2=pol(n2), q2=pol(q2), kv3=pol(kv3), a2=pol(a2), lse2=pol(lse2), h2=pol(h2),
                       st3=pol(st3), f=f)
             if lo:
                 sv.update(u_qkv=u_qkv, u_o1=u_o1, u_q2=u_q2, u_kv2=u_kv2, u_o2=u_o2)
@@ -490,7 +501,7 @@ class BasicTransformerBlock(nn.Module):
             _lin_dw(fg, o2, dh2, sv["a2"])
         enc = rt.enc
         Se = enc.shape[0] // B
-        kv3 = sv["kv2"].view(B, Se, 2 * C)
+        kv3 = sv["kv3"]
         dkv2 = torch.empty((B * Se, 2 * C), device=dh3.device, dtype=BF16)
         dk3 = dkv2.view(B, Se, 2 * C)
         dq2, _, _ = K.attention_bwd(sv["q2"].view(B, S, C), kv3[..., :C], kv3[..., C:], sv["a2"].view(B, S, C),
@@ -920,6 +931,19 @@ class UNet2DConditionModel(nn.Module):
             m._temb_off = off
             off += m.cout
         self._temb_n = off
+        # Cross-attention K/V: every transformer block projects the SAME 77 text tokens, so the blocks of one width run
+        # their K/V projections as ONE GEMM (weights concatenated here, each block's w_kv a row view of them): 2 launches
+        # per pass instead of 2 per block (the LoRA k/v down-projections likewise, see refresh_lora)
+        groups = {}
+        for _, blk in self._attn_modules():
+            groups.setdefault(blk.dim, []).append(blk)
+        self._kv_groups = {}
+        for C, lst in groups.items():
+            W = torch.cat([b.attn2.w_kv for b in lst], 0)
+            for j, b in enumerate(lst):
+                b.attn2.w_kv = W[j * 2 * C:(j + 1) * 2 * C]
+                b._kv_slot = j
+            self._kv_groups[C] = SimpleNamespace(W=W, blocks=lst)
         self.conv_in.prepare()
         self.conv_out.prepare()
         if self.full is not None:
@@ -934,11 +958,32 @@ class UNet2DConditionModel(nn.Module):
     def refresh_lora(self):
         self.lora.refresh()
 
+    def kv_text(self, rt, C):
+        """K/V of the text tokens for every block of width C: ([rows, n*2C], LoRA down-projection [policy rows, n*2r]
+        or None), computed on first use in a pass (rt.enc is then final: the paired duplication precedes every
+        transformer block).  Output column group j (C columns: k or v of block j // 2) takes the LoRA tail
+        u[:, j*r:(j+1)*r] (sB)^T -- the per-block grouped tail of the unbatched form, block after block."""
+        hit = rt.kv_cache.get(C)
+        if hit is not None:
+            return hit
+        grp = self._kv_groups[C]
+        enc = rt.enc
+        if rt.lora_on:
+            A, sB = self.lora.kv_stacks[C][:2]  # same block order as grp.W (both follow _attn_modules)
+            u = K.gemm(rt.pol(enc), A)
+            kv = K.gemm(enc, grp.W, a2=u, w2=sB, tail_group_n=C, tail_rows=enc.shape[0] // 2 if rt.paired else 0)
+        else:
+            u, kv = None, K.gemm(enc, grp.W)
+        rt.kv_cache[C] = (kv, u)
+        return kv, u
+
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
         rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=K.SideStream(),
                              fg=self.full if save else None)
         rt.pol = lambda t: t[:t.shape[0] // 2] if rt.paired else t
+        rt.kv_cache = {}
+        rt.kv_text = lambda C: self.kv_text(rt, C)
         rt.lora = self.lora
         rt.r = self.lora.r if lora_on else 0
         return rt
