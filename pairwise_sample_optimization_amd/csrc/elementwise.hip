@@ -60,8 +60,10 @@ __global__ void geglu_bwd_kernel(long M, int F, const bf16_t* __restrict__ in, l
     unpack8e(*reinterpret_cast<const uint4*>(dout + m * lddo + c), d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      dh[j] = d[j] * gelu_erf(g[j]);
-      dg[j] = d[j] * h[j] * gelu_erf_grad(g[j]);
+      float c, e;
+      gelu_erf_parts(g[j], c, e);
+      dh[j] = d[j] * g[j] * c;
+      dg[j] = d[j] * h[j] * (c + 0.39894228040143268f * g[j] * e);
     }
     *reinterpret_cast<uint4*>(din + m * lddi + c) = pack8e(dh);
     *reinterpret_cast<uint4*>(din + m * lddi + F + c) = pack8e(dg);

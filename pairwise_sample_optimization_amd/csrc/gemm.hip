@@ -512,8 +512,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           const float d0 = bf2f(dw[e] & 0xffff), d1 = bf2f(dw[e] >> 16);
           const float h0 = bf2f(hw[e] & 0xffff), h1 = bf2f(hw[e] >> 16);
           const float g0 = bf2f(gw[e] & 0xffff), g1 = bf2f(gw[e] >> 16);
-          oh[e] = pack2bf(d0 * gelu_erf(g0), d1 * gelu_erf(g1));
-          og[e] = pack2bf(d0 * h0 * gelu_erf_grad(g0), d1 * h1 * gelu_erf_grad(g1));
+          float c0, e0, c1, e1;
+          gelu_erf_parts(g0, c0, e0);
+          gelu_erf_parts(g1, c1, e1);
+          oh[e] = pack2bf(d0 * g0 * c0, d1 * g1 * c1);
+          og[e] = pack2bf(d0 * h0 * (c0 + 0.39894228040143268f * g0 * e0), d1 * h1 * (c1 + 0.39894228040143268f * g1 * e1));
         }
         bf16_t* p = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
         *reinterpret_cast<uint4*>(p) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
