@@ -676,7 +676,8 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // 256 queries per workgroup (4 x 64-row waves) when that still gives >= 2 rounds of the 512 co-resident
   // workgroups, else 128 (4 x 32): fewer K/V LDS bytes per MFMA vs. a fuller grid
   const int nq4 = cdiv(Sq, 256), nq2 = cdiv(Sq, 128);
-  const bool big = g_attn_fwd_variant == 4 || (g_attn_fwd_variant == 0 && (long)nq4 * H * B >= 1024);
+  // cross-attention (77 keys: two key tiles) keeps 128: its per-workgroup set-up outweighs the K/V reuse (-10 %)
+  const bool big = g_attn_fwd_variant == 4 || (g_attn_fwd_variant == 0 && (long)nq4 * H * B >= 1024 && Sk > 128);
   if (g_attn_vsum) {
     if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
     else attn_fwd_kernel<2, false><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);

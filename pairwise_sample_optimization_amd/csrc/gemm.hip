@@ -182,7 +182,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   const int m0 = bm * BM, n0 = bn * BN;
 
   const int nt1 = (g.K1 + BK - 1) / BK;
-  const int nt2 = g.a2 ? (g.K2 + BK - 1) / BK : 0;
+  // tiles made only of rows >= tail_m (the reference half of a paired pass) skip the LoRA K-tail: it is zero there
+  const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + BK - 1) / BK : 0;
   const int nt_all = nt1 + nt2;
   // split-K (gridDim.y > 1): this block owns K-tiles [t_beg, t_end); partials are added atomically (f32 out)
   const int per = (nt_all + gridDim.y - 1) / gridDim.y;
