@@ -389,31 +389,40 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   int cur = 0;
-  for (int t = 0; t < nt; ++t) {
+  auto mfma_half = [&](const bf16_t* la, const bf16_t* lb, int kk) {
+    bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / WM) + i * 16 + fr, kk * 4 + fk));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / WN) + j * 16 + fr, kk * 4 + fk));
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // a LoRA K-tail of rank <= 32 fills only the first 32-deep half of its (last) K-tile, the rest being zero padding:
+  // that tile is peeled off the loop and multiplies its first half only
+  const bool half_last = nt > 0 && nt2 == 1 && g.K2 <= 32 && t_end == nt_all;
+  const int nt_loop = nt - (half_last ? 1 : 0);
+  for (int t = 0; t < nt_loop; ++t) {
     const bool ahead = t + STAGES - 1 < nt;
     if (ahead) issue_tile(t + STAGES - 1, (cur + STAGES - 1) % STAGES);
     const bf16_t* la = stage_ptr(cur);
     const bf16_t* lb = stage_ptr(cur) + BM * BK;
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[MI], bfr[NJ];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * (BM / WM) + i * 16 + fr, kk * 4 + fk));
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * (BN / WN) + j * 16 + fr, kk * 4 + fk));
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+    for (int kk = 0; kk < BK / 32; ++kk) mfma_half(la, lb, kk);
     // K-tile t+1 must have landed (every wave's pieces) before anyone reads it; tiles beyond stay in flight
     if (STAGES == 3 && ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     cur = (cur + 1 == STAGES) ? 0 : cur + 1;
+  }
+  if (half_last) {  // landed: the last loop iteration waited for it (vmcnt(0): nothing was issued beyond it)
+    mfma_half(stage_ptr(cur), stage_ptr(cur) + BM * BK, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   }  // !PIPE
 
