@@ -33,9 +33,16 @@ __global__ void sqnorm_partial_kernel(long n, const float* __restrict__ g, doubl
 // out[0] = ||g * scale||_2, out[1] = clip coefficient (1 if max_norm <= 0)
 __global__ void clip_coef_kernel(int nparts, const double* __restrict__ part, float scale, float max_norm,
                                  float* __restrict__ out) {
+  // one workgroup sums the per-block partials (fixed order: strided per thread, then wave and workgroup trees)
+  __shared__ double red[OPT_THREADS / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  acc = warp_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
   if (threadIdx.x == 0) {
     double s = 0.0;
-    for (int i = 0; i < nparts; ++i) s += part[i];
+    for (int w = 0; w < OPT_THREADS / 64; ++w) s += red[w];
     const float norm = (float)sqrt(s) * scale;
     out[0] = norm;
     float c = 1.0f;
@@ -112,7 +119,7 @@ int pso_grad_clip_coef(long n, const float* grad, float grad_scale, float max_no
   hipStream_t st = (hipStream_t)stream;
   const int nb = nblocks(n);
   sqnorm_partial_kernel<<<nb, OPT_THREADS, 0, st>>>(n, grad, (double*)ws);
-  clip_coef_kernel<<<1, 64, 0, st>>>(nb, (const double*)ws, grad_scale, max_norm, out_norm_coef);
+  clip_coef_kernel<<<1, OPT_THREADS, 0, st>>>(nb, (const double*)ws, grad_scale, max_norm, out_norm_coef);
   return pso_check_launch("pso_grad_clip_coef");
 }
 
