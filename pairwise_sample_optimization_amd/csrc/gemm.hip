@@ -756,12 +756,15 @@ static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
+// raster group rows: C2-step sweep (tools/_var_ab.sh, same box) 2 / 3 / 4 / 5 / 6 / 8 / 16 -> 240.4 / 239.7 / 239.1 /
+// 239.2 / 238.9 / 240.5 / 241.9 ms
+#define PSO_GEMM_GROUP_M 4
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
   const int gv = gv_raw == 41 ? 0 : gv_raw;  // 41 = automatic dispatch with the per-lane epilogue
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
-  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
     pso_set_error("pso_gemm: tail_group_n must be a multiple of 64");
     return PSO_ERR_ARG;
@@ -1036,7 +1039,7 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   g.out2 = out_pre; g.ldo2 = ld_pre;
   g.tail_m = (pre_rows > 0 && pre_rows < M) ? pre_rows : M;
   g.vec_ok = 1; g.rows_per_group = 1;
-  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   // variant 32: the 8-phase kernel (gemm8p.hip; K % 128 == 0).  Measured equal on the UNet GEGLU shapes (16384 x
   // 10240 x 1280: 877 vs 879 TF/s; 65536 x 5120 x 640: 701 vs 697), so the 2-phase 256x256 kernel stays the default.
   if (g_gemm_variant == 32 && (K % 128) == 0 && (long)M * lda < (1L << 30) && (long)N * ldw < (1L << 30))
@@ -1065,7 +1068,7 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   g.out = out; g.ldo = ldo; g.out_dtype = PSO_BF16;
   g.aux = (const bf16_t*)pre; g.ldaux = ld_pre;
   g.vec_ok = 1; g.rows_per_group = 1;
-  g.group_m = g_gemm_group > 0 ? g_gemm_group : 8;
+  g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   const hipStream_t st = (hipStream_t)stream;
   const long t160 = (long)((M + 127) / 128) * ((N + 159) / 160);
   if ((N % 160) == 0 && t160 >= 256) return launch<128, 160, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);
