@@ -8,12 +8,17 @@ micro-step trains 2P images (2P policy UNet fwd+bwd + 2P reference fwd + fused l
 SDXL weights (seeded), N(0,1) text embeddings, trajectories from this build's own sampler (untimed), U(0,1)
 rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling), RCCL all-reduce of the flat LoRA grads.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (torchrun sets RANK/WORLD_SIZE/LOCAL_RANK)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  Under torchrun (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one rank.  Started directly with --gpus N > 1,
+  bench.py launches `python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child BEFORE any GPU call
+  and exits with its code, so both launch forms measure N GPUs.
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -159,9 +164,26 @@ def max_over_ranks(dt, dev):
     return tt.item()
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher: run N ranks under torch.distributed.run (127.0.0.1 rendezvous) as a child
+    process -- no GPU call has happened in this process -- and return its exit code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"[bench] note: WORLD_SIZE={world} but --gpus {args.gpus}; measuring the {world} launched ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")

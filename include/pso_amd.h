@@ -38,6 +38,14 @@ extern "C" {
 /* step modes */
 #define PSO_MODE_TURBO 0 /* Euler-ancestral (SDXL-Turbo)   DP/turbo_inference_with_logprob.py:24-116 */
 #define PSO_MODE_DMD 1   /* DDPM re-noise (SDXL-DMD2)      DP/distilled_inference_with_logprob.py:45-137 */
+/* DMD2 "replay" modes: the reference computes x0, the mean and the log-prob in the LATENT dtype when the latents are
+ * fp16 / bf16 (DP/distilled_inference_with_logprob.py:84-86 `.to(sample.dtype)`, :98-112 the table cast to the latent
+ * dtype, :129-135 the log-density in that dtype).  These modes round every intermediate to that
+ * dtype in the reference's operation order (values stay fp32 in memory, holding fp16 / bf16-representable numbers),
+ * and the loss stage rounds Δ, exp, the clipped ratio, its log and beta*log to it (T:844-850 on latent-dtype
+ * log-probs).  The coefficients of these modes are the latent-dtype values of the reference (pso_core.dmd_coef). */
+#define PSO_MODE_DMD_F16 2
+#define PSO_MODE_DMD_BF16 3
 
 /* Per-sample step coefficients, PSO_COEF_STRIDE floats each (host-computed in float32 from the scheduler tables):
  *   TURBO: [sigma, sigma_up, dt = sigma_down - sigma, 2*sigma_up^2, log(sigma_up), log(sqrt(2*pi)), 0, 0]
@@ -85,6 +93,17 @@ int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_pre
                       int eps_dtype, const float* coef, const float* pref, float beta, float clip_eps,
                       const float* grad_out, float grad_scale, void* deps_pol, int deps_dtype, const void* ws,
                       size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
+ * The scalar stage of the pairwise loss on given log-probs (the part of pso_pair_loss_fwd/bwd after the reductions).
+ * Replaces: T:844-850 / D:848-854 (clamp(exp(lp_theta - lp_ref), 1-eps, 1+eps), -log sigmoid(beta * sum log ratio *
+ *           pref)).mean() and its autograd gradient w.r.t. lp_theta.  torch.clamp passes the gradient AT the bounds
+ *           (mask lo <= r <= hi), which this reproduces.
+ * lp_pol, lp_ref, pref, dlp_out: [P][2] fp32 (member k of pair p at [p][k]); loss_out [1].  Same device function as
+ * the fused kernels, exposed so the clamp-boundary / tie cases can be driven with exact log-prob values.
+ * ---------------------------------------------------------------------------------------------------------------- */
+int pso_pair_loss_from_lp(int mode, int P, const float* lp_pol, const float* lp_ref, const float* pref, float beta,
+                          float clip_eps, float* loss_out, float* dlp_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * bf16 MFMA GEMM, fp32 accumulate.

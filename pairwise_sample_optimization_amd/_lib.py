@@ -16,6 +16,8 @@ PSO_F32 = 0
 PSO_BF16 = 1
 MODE_TURBO = 0
 MODE_DMD = 1
+MODE_DMD_F16 = 2   # DMD2 latent-dtype replay modes (include/pso_amd.h PSO_MODE_DMD_F16 / _BF16)
+MODE_DMD_BF16 = 3
 COEF_STRIDE = 8
 
 _lib = None
@@ -36,6 +38,7 @@ SIGNATURES = {
     "pso_pair_loss_ws_bytes": (csz, [ci, ci]),
     "pso_pair_loss_fwd": (ci, [ci, ci, ci, vp, vp, vp, vp, ci, vp, vp, cf, cf, vp, vp, vp, csz, vp]),
     "pso_pair_loss_bwd": (ci, [ci, ci, ci, vp, vp, vp, ci, vp, vp, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
+    "pso_pair_loss_from_lp": (ci, [ci, ci, vp, vp, vp, cf, cf, vp, vp, vp]),
     "pso_db_loss_ws_bytes": (csz, [ci, ci]),
     "pso_db_loss_fwd": (ci, [ci, ci, ci, vp, vp, ci, vp, vp, vp, cf, cf, cf, vp, vp, vp, vp, csz, vp]),
     "pso_db_loss_bwd": (ci, [ci, ci, ci, vp, ci, vp, vp, vp, cf, cf, cf, vp, cf, vp, ci, vp, csz, vp]),

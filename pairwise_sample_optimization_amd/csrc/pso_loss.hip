@@ -14,6 +14,18 @@
 // Element-wise op order must mirror the reference (no FMA contraction) for 1e-6 parity.
 #pragma clang fp contract(off)
 
+// DMD2 replay modes (PSO_MODE_DMD_F16 / _BF16): every intermediate of the reference's latent-dtype arithmetic is
+// rounded to that dtype (torch's CPU/GPU fp16 and bf16 element-wise ops compute in fp32 and round the result).
+template <int MODE>
+__device__ __forceinline__ float rl(float x) {
+  if constexpr (MODE == PSO_MODE_DMD_F16) return (float)(_Float16)x;
+  else if constexpr (MODE == PSO_MODE_DMD_BF16) return bf_round(x);
+  else return x;
+}
+__device__ __forceinline__ float rl_rt(int mode, float x) {
+  return mode == PSO_MODE_DMD_F16 ? rl<PSO_MODE_DMD_F16>(x) : mode == PSO_MODE_DMD_BF16 ? rl<PSO_MODE_DMD_BF16>(x) : x;
+}
+
 #define LP_CHUNK 8192
 #define LP_THREADS 256
 
@@ -35,10 +47,17 @@ __device__ __forceinline__ float step_mean(float x, float e, const Coef& k) {
     const float pred = x - s * e;
     const float deriv = (x - pred) / s;
     return x + deriv * k.c[2];
-  } else {
-    const float x0 = (x - k.c[1] * e) / k.c[0];
-    return k.c[2] * x0;
+  } else {  // DP/distilled_inference_with_logprob.py:84-86 (x0 cast to the latent dtype), :112
+    const float x0 = rl<MODE>((x - k.c[1] * e) / k.c[0]);
+    return rl<MODE>(k.c[2] * x0);
   }
+}
+// one element of the Gaussian log-density, DP/turbo_inference_with_logprob.py:108-112 / DP/distilled_...:129-133
+template <int MODE>
+__device__ __forceinline__ float lp_term(float pv, float mu, float denom, float lstd, float lc) {
+  const float d = rl<MODE>(pv - mu);
+  const float q = rl<MODE>(-rl<MODE>(d * d) / denom);
+  return rl<MODE>(rl<MODE>(q - lstd) - lc);
 }
 template <int MODE>
 __device__ __forceinline__ float step_std(const Coef& k) { return MODE == PSO_MODE_TURBO ? k.c[1] : k.c[3]; }
@@ -109,30 +128,27 @@ __global__ __launch_bounds__(LP_THREADS) void lp_partial_kernel(
       const float4 z = *reinterpret_cast<const float4*>(noise + nb);
       const float zs[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pv[j] = MODE == PSO_MODE_TURBO ? mu[j] + zs[j] * std : mu[j] + std * zs[j];
+      for (int j = 0; j < 4; ++j) pv[j] = MODE == PSO_MODE_TURBO ? mu[j] + zs[j] * std : rl<MODE>(mu[j] + rl<MODE>(std * zs[j]));
       *reinterpret_cast<float4*>(prev_out + base + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float d = pv[j] - mu[j];
-      const float t = -(d * d) / denom - lstd - lc;
-      acc += (double)t;
-    }
+    for (int j = 0; j < 4; ++j) acc += (double)lp_term<MODE>(pv[j], mu[j], denom, lstd, lc);
   }
   const double s = block_sum_d(acc, red);
   if (threadIdx.x == 0) partial[(size_t)combo * gridDim.x + blockIdx.x] = s;
 }
 
-__device__ __forceinline__ float lp_from_partials(const double* partial, int combo, int nchunks, int n) {
+// the mean over C,H,W (the latent-dtype result of .mean() in the replay modes)
+__device__ __forceinline__ float lp_from_partials(int mode, const double* partial, int combo, int nchunks, int n) {
   double s = 0.0;
   for (int c = 0; c < nchunks; ++c) s += partial[(size_t)combo * nchunks + c];
-  return (float)(s / (double)n);
+  return rl_rt(mode, (float)(s / (double)n));
 }
 
-__global__ void lp_finalize_kernel(int B, int n, int nchunks, const double* __restrict__ partial,
+__global__ void lp_finalize_kernel(int mode, int B, int n, int nchunks, const double* __restrict__ partial,
                                    float* __restrict__ log_prob) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) log_prob[b] = lp_from_partials(partial, b, nchunks, n);
+  if (b < B) log_prob[b] = lp_from_partials(mode, partial, b, nchunks, n);
 }
 
 struct PairScalars {
@@ -141,25 +157,27 @@ struct PairScalars {
   float loss;      // -log sigmoid(z) of this pair
 };
 
-__device__ __forceinline__ PairScalars pair_scalars(const double* partial, int p, int P, int nchunks, int n,
-                                                    const float* pref, float beta, float clip_eps,
-                                                    float grad_scale) {
+// T:844-850 on the four log-probs of pair p.  Replay modes round Δ, exp(Δ), the clamped ratio, its log and beta*log
+// to the latent dtype (the reference's log-probs are latent-dtype tensors there); pref is fp32, so z and the rest stay
+// fp32.  torch.clamp's backward passes the gradient where lo <= r <= hi (bounds included).
+__device__ __forceinline__ PairScalars pair_scalars_lp(int mode, const float (&lp)[2][2], float p0, float p1, int P,
+                                                       float beta, float clip_eps, float grad_scale) {
   PairScalars s;
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int w = 0; w < 2; ++w) s.lp[m][w] = lp_from_partials(partial, 2 * (2 * p + m) + w, nchunks, n);
+  for (int m = 0; m < 2; ++m) {
+    s.lp[m][0] = lp[m][0];
+    s.lp[m][1] = lp[m][1];
+  }
   const float lo = 1.0f - clip_eps, hi = 1.0f + clip_eps;
   float lr[2];
   bool inside[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const float r = expf(s.lp[m][0] - s.lp[m][1]);
-    inside[m] = (r > lo) && (r < hi);
-    lr[m] = logf(fminf(fmaxf(r, lo), hi));
+    const float r = rl_rt(mode, expf(rl_rt(mode, lp[m][0] - lp[m][1])));
+    inside[m] = (r >= lo) && (r <= hi);
+    lr[m] = rl_rt(mode, beta * rl_rt(mode, logf(rl_rt(mode, fminf(fmaxf(r, lo), hi)))));
   }
-  const float p0 = pref[2 * p], p1 = pref[2 * p + 1];
-  const float z = beta * lr[0] * p0 + beta * lr[1] * p1;
+  const float z = lr[0] * p0 + lr[1] * p1;
   const float sig = 1.0f / (1.0f + expf(-z));
   s.loss = -logf(sig);
   const float common = -(1.0f - sig) * beta / (float)P * grad_scale;
@@ -168,13 +186,24 @@ __device__ __forceinline__ PairScalars pair_scalars(const double* partial, int p
   return s;
 }
 
+__device__ __forceinline__ PairScalars pair_scalars(int mode, const double* partial, int p, int P, int nchunks, int n,
+                                                    const float* pref, float beta, float clip_eps,
+                                                    float grad_scale) {
+  float lp[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int w = 0; w < 2; ++w) lp[m][w] = lp_from_partials(mode, partial, 2 * (2 * p + m) + w, nchunks, n);
+  return pair_scalars_lp(mode, lp, pref[2 * p], pref[2 * p + 1], P, beta, clip_eps, grad_scale);
+}
+
 // Forward finalize: one thread per pair writes lp_out and the per-pair loss; thread 0 then averages (fixed order).
-__global__ void pair_loss_finalize_kernel(int P, int n, int nchunks, const float* __restrict__ pref, float beta,
-                                          float clip_eps, const double* __restrict__ partial,
+__global__ void pair_loss_finalize_kernel(int mode, int P, int n, int nchunks, const float* __restrict__ pref,
+                                          float beta, float clip_eps, const double* __restrict__ partial,
                                           float* __restrict__ lp_out, float* __restrict__ loss_out) {
   __shared__ float pair_loss_sh[1024];
   for (int q = threadIdx.x; q < P; q += blockDim.x) {
-    const PairScalars s = pair_scalars(partial, q, P, nchunks, n, pref, beta, clip_eps, 1.0f);
+    const PairScalars s = pair_scalars(mode, partial, q, P, nchunks, n, pref, beta, clip_eps, 1.0f);
     pair_loss_sh[q & 1023] = s.loss;
     for (int mm = 0; mm < 2; ++mm) {
       lp_out[(2 * q + mm) * 2 + 0] = s.lp[mm][0];
@@ -202,7 +231,7 @@ __global__ __launch_bounds__(LP_THREADS) void pair_grad_kernel(
   __shared__ float g_sh;
   if (threadIdx.x == 0) {
     const float up = grad_out ? grad_out[0] * grad_scale : grad_scale;
-    g_sh = pair_scalars(partial, p, P, nchunks, n, pref, beta, clip_eps, up).g[m];
+    g_sh = pair_scalars(MODE, partial, p, P, nchunks, n, pref, beta, clip_eps, up).g[m];
   }
   __syncthreads();
   const Coef k = load_coef(coef, img);
@@ -229,6 +258,37 @@ __global__ __launch_bounds__(LP_THREADS) void pair_grad_kernel(
   }
 }
 
+__global__ void pair_loss_lp_kernel(int mode, int P, const float* __restrict__ lp_pol, const float* __restrict__ lp_ref,
+                                    const float* __restrict__ pref, float beta, float clip_eps,
+                                    float* __restrict__ loss_out, float* __restrict__ dlp_out) {
+  __shared__ float pair_loss_sh[1024];
+  for (int q = threadIdx.x; q < P; q += blockDim.x) {
+    const float lp[2][2] = {{lp_pol[2 * q], lp_ref[2 * q]}, {lp_pol[2 * q + 1], lp_ref[2 * q + 1]}};
+    const PairScalars s = pair_scalars_lp(mode, lp, pref[2 * q], pref[2 * q + 1], P, beta, clip_eps, 1.0f);
+    pair_loss_sh[q] = s.loss;
+    if (dlp_out) {
+      dlp_out[2 * q] = s.g[0];
+      dlp_out[2 * q + 1] = s.g[1];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double L = 0.0;
+    for (int q = 0; q < P; ++q) L += (double)pair_loss_sh[q];
+    loss_out[0] = (float)(L / (double)P);
+  }
+}
+
+#define PSO_MODE_OK(m) ((m) == PSO_MODE_TURBO || (m) == PSO_MODE_DMD || (m) == PSO_MODE_DMD_F16 || (m) == PSO_MODE_DMD_BF16)
+// mode -> template instantiation
+#define PSO_MODE_DISPATCH(mode, KERNEL_CALL)                       \
+  switch (mode) {                                                  \
+    case PSO_MODE_TURBO: { constexpr int M_ = PSO_MODE_TURBO; KERNEL_CALL; } break; \
+    case PSO_MODE_DMD: { constexpr int M_ = PSO_MODE_DMD; KERNEL_CALL; } break;     \
+    case PSO_MODE_DMD_F16: { constexpr int M_ = PSO_MODE_DMD_F16; KERNEL_CALL; } break; \
+    default: { constexpr int M_ = PSO_MODE_DMD_BF16; KERNEL_CALL; } break;           \
+  }
+
 extern "C" {
 
 size_t pso_step_logprob_ws_bytes(int B, int n) { return (size_t)B * cdiv(n, LP_CHUNK) * sizeof(double); }
@@ -237,7 +297,7 @@ size_t pso_pair_loss_ws_bytes(int P, int n) { return (size_t)4 * P * cdiv(n, LP_
 int pso_step_logprob(int mode, int B, int n, const float* sample, const void* eps, int eps_dtype,
                      const float* prev_in, const float* noise, int noise_shared, const float* coef,
                      float* prev_out, float* log_prob, void* ws, size_t ws_bytes, void* stream) {
-  PSO_ARG_CHECK(mode == PSO_MODE_TURBO || mode == PSO_MODE_DMD, "pso_step_logprob: bad mode %d", mode);
+  PSO_ARG_CHECK(PSO_MODE_OK(mode), "pso_step_logprob: bad mode %d", mode);
   PSO_ARG_CHECK(B > 0 && n > 0 && (n % 4) == 0, "pso_step_logprob: need B>0, n>0, n%%4==0 (B=%d n=%d)", B, n);
   PSO_ARG_CHECK(sample && eps && coef && log_prob, "pso_step_logprob: null pointer");
   PSO_ARG_CHECK(prev_in || (noise && prev_out), "pso_step_logprob: need prev_in, or noise and prev_out");
@@ -247,20 +307,17 @@ int pso_step_logprob(int mode, int B, int n, const float* sample, const void* ep
   const int nchunks = cdiv(n, LP_CHUNK);
   double* partial = (double*)ws;
   dim3 grid(nchunks, B);
-  if (mode == PSO_MODE_TURBO)
-    lp_partial_kernel<PSO_MODE_TURBO, false><<<grid, LP_THREADS, 0, st>>>(
-        n, sample, prev_in, eps, nullptr, eps_dtype, noise, noise_shared, coef, prev_out, partial);
-  else
-    lp_partial_kernel<PSO_MODE_DMD, false><<<grid, LP_THREADS, 0, st>>>(
-        n, sample, prev_in, eps, nullptr, eps_dtype, noise, noise_shared, coef, prev_out, partial);
-  lp_finalize_kernel<<<cdiv(B, 64), 64, 0, st>>>(B, n, nchunks, partial, log_prob);
+  PSO_MODE_DISPATCH(mode, (lp_partial_kernel<M_, false><<<grid, LP_THREADS, 0, st>>>(
+                              n, sample, prev_in, eps, nullptr, eps_dtype, noise, noise_shared, coef, prev_out,
+                              partial)))
+  lp_finalize_kernel<<<cdiv(B, 64), 64, 0, st>>>(mode, B, n, nchunks, partial, log_prob);
   return pso_check_launch("pso_step_logprob");
 }
 
 int pso_pair_loss_fwd(int mode, int P, int n, const float* x, const float* x_prev, const void* eps_pol,
                       const void* eps_ref, int eps_dtype, const float* coef, const float* pref, float beta,
                       float clip_eps, float* lp_out, float* loss_out, void* ws, size_t ws_bytes, void* stream) {
-  PSO_ARG_CHECK(mode == PSO_MODE_TURBO || mode == PSO_MODE_DMD, "pso_pair_loss_fwd: bad mode %d", mode);
+  PSO_ARG_CHECK(PSO_MODE_OK(mode), "pso_pair_loss_fwd: bad mode %d", mode);
   PSO_ARG_CHECK(P > 0 && P <= 1024 && n > 0 && (n % 4) == 0,
                 "pso_pair_loss_fwd: need 0<P<=1024, n>0, n%%4==0 (P=%d n=%d)", P, n);
   PSO_ARG_CHECK(x && x_prev && eps_pol && eps_ref && coef && pref && lp_out && loss_out,
@@ -271,13 +328,9 @@ int pso_pair_loss_fwd(int mode, int P, int n, const float* x, const float* x_pre
   const int nchunks = cdiv(n, LP_CHUNK);
   double* partial = (double*)ws;
   dim3 g1(nchunks, 4 * P);
-  if (mode == PSO_MODE_TURBO)
-    lp_partial_kernel<PSO_MODE_TURBO, true><<<g1, LP_THREADS, 0, st>>>(
-        n, x, x_prev, eps_pol, eps_ref, eps_dtype, nullptr, 0, coef, nullptr, partial);
-  else
-    lp_partial_kernel<PSO_MODE_DMD, true><<<g1, LP_THREADS, 0, st>>>(
-        n, x, x_prev, eps_pol, eps_ref, eps_dtype, nullptr, 0, coef, nullptr, partial);
-  pair_loss_finalize_kernel<<<1, 256, 0, st>>>(P, n, nchunks, pref, beta, clip_eps, partial, lp_out, loss_out);
+  PSO_MODE_DISPATCH(mode, (lp_partial_kernel<M_, true><<<g1, LP_THREADS, 0, st>>>(
+                              n, x, x_prev, eps_pol, eps_ref, eps_dtype, nullptr, 0, coef, nullptr, partial)))
+  pair_loss_finalize_kernel<<<1, 256, 0, st>>>(mode, P, n, nchunks, pref, beta, clip_eps, partial, lp_out, loss_out);
   return pso_check_launch("pso_pair_loss_fwd");
 }
 
@@ -285,7 +338,7 @@ int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_pre
                       int eps_dtype, const float* coef, const float* pref, float beta, float clip_eps,
                       const float* grad_out, float grad_scale, void* deps_pol, int deps_dtype, const void* ws,
                       size_t ws_bytes, void* stream) {
-  PSO_ARG_CHECK(mode == PSO_MODE_TURBO || mode == PSO_MODE_DMD, "pso_pair_loss_bwd: bad mode %d", mode);
+  PSO_ARG_CHECK(PSO_MODE_OK(mode), "pso_pair_loss_bwd: bad mode %d", mode);
   PSO_ARG_CHECK(P > 0 && n > 0 && (n % 4) == 0, "pso_pair_loss_bwd: need P>0, n>0, n%%4==0");
   PSO_ARG_CHECK(x && x_prev && eps_pol && coef && pref && deps_pol, "pso_pair_loss_bwd: null pointer");
   PSO_ARG_CHECK(eps_dtype == PSO_F32 || eps_dtype == PSO_BF16, "pso_pair_loss_bwd: bad eps dtype");
@@ -295,15 +348,20 @@ int pso_pair_loss_bwd(int mode, int P, int n, const float* x, const float* x_pre
   const int nchunks = cdiv(n, LP_CHUNK);
   const double* partial = (const double*)ws;
   dim3 g2(nchunks, 2 * P);
-  if (mode == PSO_MODE_TURBO)
-    pair_grad_kernel<PSO_MODE_TURBO><<<g2, LP_THREADS, 0, st>>>(P, n, nchunks, x, x_prev, eps_pol, eps_dtype, coef,
-                                                                pref, beta, clip_eps, grad_out, grad_scale, partial,
-                                                                deps_pol, deps_dtype);
-  else
-    pair_grad_kernel<PSO_MODE_DMD><<<g2, LP_THREADS, 0, st>>>(P, n, nchunks, x, x_prev, eps_pol, eps_dtype, coef,
-                                                              pref, beta, clip_eps, grad_out, grad_scale, partial,
-                                                              deps_pol, deps_dtype);
+  PSO_MODE_DISPATCH(mode, (pair_grad_kernel<M_><<<g2, LP_THREADS, 0, st>>>(
+                              P, n, nchunks, x, x_prev, eps_pol, eps_dtype, coef, pref, beta, clip_eps, grad_out,
+                              grad_scale, partial, deps_pol, deps_dtype)))
   return pso_check_launch("pso_pair_loss_bwd");
+}
+
+int pso_pair_loss_from_lp(int mode, int P, const float* lp_pol, const float* lp_ref, const float* pref, float beta,
+                          float clip_eps, float* loss_out, float* dlp_out, void* stream) {
+  PSO_ARG_CHECK(PSO_MODE_OK(mode), "pso_pair_loss_from_lp: bad mode %d", mode);
+  PSO_ARG_CHECK(P > 0 && P <= 1024, "pso_pair_loss_from_lp: need 0 < P <= 1024 (P=%d)", P);
+  PSO_ARG_CHECK(lp_pol && lp_ref && pref && loss_out, "pso_pair_loss_from_lp: null pointer");
+  pair_loss_lp_kernel<<<1, 256, 0, (hipStream_t)stream>>>(mode, P, lp_pol, lp_ref, pref, beta, clip_eps, loss_out,
+                                                          dlp_out);
+  return pso_check_launch("pso_pair_loss_from_lp");
 }
 
 }  // extern "C"

@@ -238,7 +238,33 @@ def pair_loss_ws(P, n, device):
     return torch.empty(lib().pso_pair_loss_ws_bytes(P, n), device=device, dtype=torch.uint8)
 
 
+def _check_pair_operands(x, x_prev, eps_pol, coef, pref, eps_ref=None):
+    """Shape / dtype / layout contract of pso_pair_loss_fwd/bwd (the C-ABI reads raw pointers): x, x_prev fp32
+    contiguous [2P, ...]; eps in one dtype (fp32 or bf16), contiguous, same shape; coef fp32 [2P, 8]; pref fp32 [P, 2]."""
+    require_cuda(x, x_prev, eps_pol, eps_ref, coef, pref)
+    if x.dtype != torch.float32 or x_prev.dtype != torch.float32:
+        raise _lib.PsoLibError("pair loss: x / x_prev must be float32")
+    if x.shape != x_prev.shape or x.shape != eps_pol.shape or (eps_ref is not None and eps_ref.shape != x.shape):
+        raise _lib.PsoLibError(f"pair loss: shape mismatch x {tuple(x.shape)} x_prev {tuple(x_prev.shape)} "
+                               f"eps_pol {tuple(eps_pol.shape)}" +
+                               (f" eps_ref {tuple(eps_ref.shape)}" if eps_ref is not None else ""))
+    if eps_ref is not None and eps_ref.dtype != eps_pol.dtype:
+        raise _lib.PsoLibError(f"pair loss: eps_pol {eps_pol.dtype} and eps_ref {eps_ref.dtype} differ")
+    dtype_code(eps_pol)
+    if x.shape[0] % 2:
+        raise _lib.PsoLibError("pair loss: batch must be 2P images (pair p, member k at row 2p + k)")
+    P = x.shape[0] // 2
+    if coef.dtype != torch.float32 or tuple(coef.shape) != (2 * P, _lib.COEF_STRIDE):
+        raise _lib.PsoLibError(f"pair loss: coef must be float32 [{2 * P}, {_lib.COEF_STRIDE}]")
+    if pref.dtype != torch.float32 or tuple(pref.shape) != (P, 2):
+        raise _lib.PsoLibError(f"pair loss: pref must be float32 [{P}, 2]")
+    for t in (x, x_prev, eps_pol, eps_ref, coef, pref):
+        if t is not None and not t.is_contiguous():
+            raise _lib.PsoLibError("pair loss: operands must be contiguous")
+
+
 def pair_loss_fwd(mode, x, x_prev, eps_pol, eps_ref, coef, pref, beta, clip_eps, ws):
+    _check_pair_operands(x, x_prev, eps_pol, coef, pref, eps_ref)
     P = x.shape[0] // 2
     n = x[0].numel()
     lp = torch.empty((2 * P, 2), device=x.device, dtype=torch.float32)
@@ -251,6 +277,7 @@ def pair_loss_fwd(mode, x, x_prev, eps_pol, eps_ref, coef, pref, beta, clip_eps,
 
 def pair_loss_bwd(mode, x, x_prev, eps_pol, coef, pref, beta, clip_eps, ws, grad_out=None, grad_scale=1.0,
                   out_dtype=BF16):
+    _check_pair_operands(x, x_prev, eps_pol, coef, pref)
     P = x.shape[0] // 2
     n = x[0].numel()
     deps = torch.empty(eps_pol.shape, device=x.device, dtype=out_dtype)
@@ -259,6 +286,20 @@ def pair_loss_bwd(mode, x, x_prev, eps_pol, coef, pref, beta, clip_eps, ws, grad
                                   ptr(deps), dtype_code(deps), ptr(ws), ws.numel(), stream_ptr()),
           "pso_pair_loss_bwd")
     return deps
+
+
+def pair_loss_from_lp(mode, lp_pol, lp_ref, pref, beta, clip_eps):
+    """T:844-850 on given log-probs lp_pol / lp_ref / pref [P, 2] fp32 -> (loss, dL/d lp_pol [P, 2])."""
+    require_cuda(lp_pol, lp_ref, pref)
+    P = lp_pol.shape[0]
+    for t in (lp_pol, lp_ref, pref):
+        assert t.dtype == torch.float32 and tuple(t.shape) == (P, 2)
+    loss = torch.empty((), device=lp_pol.device, dtype=torch.float32)
+    dlp = torch.empty((P, 2), device=lp_pol.device, dtype=torch.float32)
+    check(lib().pso_pair_loss_from_lp(mode, P, ptr(lp_pol.contiguous()), ptr(lp_ref.contiguous()),
+                                      ptr(pref.contiguous()), float(beta), float(clip_eps), ptr(loss), ptr(dlp),
+                                      stream_ptr()), "pso_pair_loss_from_lp")
+    return loss, dlp
 
 
 DB_SIGMOID, DB_HINGE = 0, 1  # PSO_DB_* ("pso", "pso_db")
@@ -585,6 +626,8 @@ def preference(rewards, mode, reward_idx=None, out=None):
     """rewards [P, 2, m] fp32 -> pref [P, 2]."""
     P, _, m = rewards.shape
     out = torch.empty((P, 2), device=rewards.device, dtype=torch.float32) if out is None else out
+    if reward_idx is not None:
+        reward_idx = reward_idx.to(torch.int64).contiguous()
     check(lib().pso_preference(P, m, ptr(rewards.float().contiguous()), ptr(reward_idx), int(mode), ptr(out),
                                stream_ptr()), "pso_preference")
     return out

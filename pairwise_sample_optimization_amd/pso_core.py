@@ -12,7 +12,7 @@ import math
 import torch
 
 from . import kernels as K
-from ._lib import MODE_TURBO, MODE_DMD, COEF_STRIDE
+from ._lib import MODE_TURBO, MODE_DMD, MODE_DMD_F16, MODE_DMD_BF16, COEF_STRIDE
 
 LOG_SQRT_2PI = torch.log(torch.sqrt(2 * torch.as_tensor(math.pi))).item()  # same float as the reference's expression
 
@@ -42,12 +42,38 @@ def turbo_coef(sigmas, timesteps, t):
     return c
 
 
-def dmd_coef(alphas_cumprod, t, t_prev):
+DMD_REPLAY_MODES = {torch.float16: MODE_DMD_F16, torch.bfloat16: MODE_DMD_BF16}
+
+
+def dmd_mode(latent_dtype=torch.float32):
+    """Kernel mode of a DMD2 step on latents of `latent_dtype` (fp16 / bf16 -> the latent-dtype replay modes)."""
+    return DMD_REPLAY_MODES.get(latent_dtype, MODE_DMD)
+
+
+def dmd_coef(alphas_cumprod, t, t_prev, latent_dtype=torch.float32):
     """Per-sample [sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev), 2(1-a_prev), log sqrt(1-a_prev),
-    log sqrt(2 pi), 0] (float32, the reference's `** 0.5` on the float32 table)."""
+    log sqrt(2 pi), 0] (float32, the reference's `** 0.5` on the float32 table).  latent_dtype fp16 / bf16: entries
+    2-5 are the reference's latent-dtype values (DP/distilled_inference_with_logprob.py:98-110 casts the table to the
+    latent dtype, then every op rounds to it) -- the same torch CPU ops on the same dtype."""
     ac = _f32(alphas_cumprod)
     a_t = ac[torch.as_tensor(t).reshape(-1).long().cpu()]
-    a_p = ac[torch.as_tensor(t_prev).reshape(-1).long().cpu()]
+    tp = torch.as_tensor(t_prev).reshape(-1).long().cpu()
+    a_p = ac[tp]
+    if latent_dtype in DMD_REPLAY_MODES:
+        acl = ac.to(latent_dtype)
+        sa_l = acl[tp] ** 0.5
+        sb_l = (1 - acl[tp]) ** 0.5
+        c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
+        c[:, 0] = a_t ** 0.5
+        c[:, 1] = (1 - a_t) ** 0.5
+        c[:, 2] = sa_l.float()
+        c[:, 3] = sb_l.float()
+        c[:, 4] = (2 * (sb_l ** 2)).float()
+        c[:, 5] = torch.log(sb_l).float()
+        # `- torch.log(torch.sqrt(2 * torch.as_tensor(math.pi)))` (:132): the fp32 0-dim tensor meets a latent-dtype
+        # tensor and is cast to that dtype first
+        c[:, 6] = torch.tensor(LOG_SQRT_2PI).to(latent_dtype).float()
+        return c
     sbp = (1 - a_p) ** 0.5
     c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
     c[:, 0] = a_t ** 0.5

@@ -70,6 +70,79 @@ def allreduce_grads(flat, process_group=None):
     return 1.0 / world
 
 
+class GradBuckets:
+    """DDP-style gradient sync overlapped with the backward (what accelerator.backward's DDP bucket hooks do on a sync
+    micro-step, T:228-233,857): the flat trained gradient is cut into ~bucket_mb contiguous buckets
+    along the backward's completion order (UNet2DConditionModel.grad_unit_ranges); backward_nhwc reports every
+    finished unit through rt.unit_done and, as soon as a bucket's last unit is done, its all-reduce (SUM) is issued
+    asynchronously -- with RCCL it runs on the communicator's own stream, ordered after the compute stream's work so
+    far, beside the rest of the backward.  finish() issues whatever is left and makes the compute stream wait for
+    every bucket before the clip / AdamW read the gradient.  The 1/world mean is folded into those kernels."""
+
+    def __init__(self, unet, flat, bucket_mb=32.0, process_group=None):
+        self.flat = flat
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group)
+        cap = int(bucket_mb * 1e6 / flat.element_size())
+        self.buckets = []        # [(offset, numel, last unit)]
+        self.unit_bucket = {}    # unit -> bucket index (every unit of the bucket)
+        units = unet.grad_unit_ranges()
+        cur_off, cur_n, cur_units = None, 0, []
+        for unit, off, n in units:
+            if cur_off is None:
+                cur_off = off
+            cur_n += n
+            cur_units.append(unit)
+            if cur_n >= cap:
+                self._close(cur_off, cur_n, cur_units)
+                cur_off, cur_n, cur_units = None, 0, []
+        if cur_units:
+            self._close(cur_off, cur_n, cur_units)
+        covered = sum(n for _, n, _ in self.buckets)
+        assert covered == flat.numel(), f"buckets cover {covered} of {flat.numel()} gradient elements"
+        self.reset()
+
+    def _close(self, off, n, units):
+        b = len(self.buckets)
+        self.buckets.append((off, n, tuple(units)))
+        for u in units:
+            self.unit_bucket[u] = b
+
+    def reset(self):
+        self.pending = [set(u) for _, _, u in self.buckets]
+        self.works = [None] * len(self.buckets)
+
+    def _issue(self, b, side=None):
+        if self.works[b] is not None:
+            return
+        if side is not None:
+            side.join()  # LoRA dW launches on the side stream belong to this bucket
+        off, n, _ = self.buckets[b]
+        self.works[b] = dist.all_reduce(self.flat[off:off + n], group=self.pg, async_op=True)
+
+    def hook(self, rt):
+        """rt.unit_done for one backward pass (the pass that ends an accumulation window)."""
+        side = getattr(rt, "side", None)
+
+        def unit_done(unit):
+            b = self.unit_bucket.get(unit)
+            if b is None:
+                return
+            self.pending[b].discard(unit)
+            if not self.pending[b]:
+                self._issue(b, side)
+        return unit_done
+
+    def finish(self):
+        """Issue the buckets not reported (none on the normal path), then wait for all of them; returns 1/world."""
+        for b in range(len(self.buckets)):
+            self._issue(b)
+        for w in self.works:
+            w.wait()
+        self.reset()
+        return 1.0 / self.world
+
+
 def trainable(unet):
     """(master, grad, refresh) of what the step trains: the flat LoRA bucket (the reference's recipe), or every UNet
     parameter when unet.enable_full_grads() was called (BASELINE C3 / C4, build-only)."""
@@ -83,9 +156,14 @@ def lora_optimizer_step(tr):
     """accelerator.backward's sync step + clip_grad_norm_ + optimizer.step + zero_grad (T:857-861, DB:1953-1964) on
     the flat LoRA bucket of tr.unet: RCCL all-reduce -> global-norm clip coefficient -> fused AdamW (clip and 1/world
     folded into the gradient read) -> zero -> refresh the bf16 working copies.  tr carries exp_avg, exp_avg_sq,
-    opt_step, clip_buf, lr, betas, adam_eps, wd, max_grad_norm, pg."""
+    opt_step, clip_buf, lr, betas, adam_eps, wd, max_grad_norm, pg and, when the last backward of the window already
+    issued the bucketed all-reduce (tr.sync_armed), the GradBuckets to finish."""
     master, grad, refresh = trainable(tr.unet)
-    scale = allreduce_grads(grad, tr.pg)
+    if getattr(tr, "sync_armed", False):
+        scale = tr.buckets.finish()
+        tr.sync_armed = False
+    else:
+        scale = allreduce_grads(grad, tr.pg)
     K.grad_clip_coef(grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
     tr.opt_step += 1
     K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
@@ -97,9 +175,15 @@ def lora_optimizer_step(tr):
 class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
-                 train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None):
+                 train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None,
+                 latent_dtype=torch.float32):
         self.unet = unet
-        self.mode = MODE_TURBO if mode == "turbo" else MODE_DMD
+        if mode not in ("turbo", "dmd"):
+            raise ValueError(f"mode must be 'turbo' or 'dmd', got {mode!r}")
+        # DMD2 with fp16 / bf16 latents: the reference's latent-dtype step / log-prob arithmetic (replay modes,
+        # DP/distilled_inference_with_logprob.py:84-135); turbo upcasts to fp32 in the reference, so it stays fp32
+        self.latent_dtype = latent_dtype if mode == "dmd" else torch.float32
+        self.mode = MODE_TURBO if mode == "turbo" else pso_core.dmd_mode(self.latent_dtype)
         self.num_steps = num_steps
         self.T = num_steps - 1                       # the last (deterministic) step is never trained (T:218-221)
         self.beta, self.clip_eps = beta, clip_eps
@@ -123,6 +207,11 @@ class PSOTrainer:
         if getattr(unet, "full", None) is not None and ref_unet is None:
             raise ValueError("full-UNet training needs ref_unet (a frozen copy of the initial weights)")
         self.loss_hist = []
+        # overlapped bucketed all-reduce on multi-GPU runs (GradBuckets); off inside hipGraph capture
+        self.overlap_sync = self.world > 1
+        self.buckets = GradBuckets(unet, trainable(unet)[1], process_group=process_group) if self.overlap_sync \
+            else None
+        self.sync_armed = False
         self.max_pass_images = max_pass_images  # images per batched UNet pass (HBM budget: ~5 GB saved each @1024^2)
         self.auto_step = True  # run the optimizer every gas*T micro-steps (tests may inspect raw grads)
         if self.mode == MODE_TURBO:
@@ -140,18 +229,21 @@ class PSOTrainer:
             if self.T > 0 else torch.zeros(0, 8, device=dev)
 
     @classmethod
-    def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None, ref_unet=None):
+    def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None, ref_unet=None,
+                    latent_dtype=torch.float32):
         """Build from a reference run config (`config_sdxl_{turbo,dmd}_dpo.get_config()`): sample.num_steps,
         train.{beta, eps, learning_rate, adam_*, max_grad_norm, gradient_accumulation_steps, batch_size}.
-        Turbo enforces `distilled_train_steps == num_steps - 1` like T:221."""
+        Both trainers require `distilled_train_steps == num_steps - 1` (turbo asserts it at T:221; DMD2 asserts
+        `<=` at D:225 and the trajectory length `==` at D:719-720)."""
         tr = config.train
-        if mode == "turbo" and tr.distilled_train_steps != config.sample.num_steps - 1:
-            raise AssertionError("train.distilled_train_steps must equal sample.num_steps - 1")
+        if tr.distilled_train_steps != config.sample.num_steps - 1:
+            raise AssertionError("train.distilled_train_steps must equal sample.num_steps - 1 "
+                                 f"({tr.distilled_train_steps} vs {config.sample.num_steps - 1})")
         return cls(unet, mode=mode, num_steps=config.sample.num_steps, beta=float(tr.beta), clip_eps=float(tr.eps),
                    lr=tr.learning_rate, betas=(tr.adam_beta1, tr.adam_beta2), weight_decay=tr.adam_weight_decay,
                    adam_eps=tr.adam_epsilon, max_grad_norm=tr.max_grad_norm,
                    gradient_accumulation_steps=tr.gradient_accumulation_steps, train_batch_size=tr.batch_size,
-                   num_reward=num_reward, process_group=process_group, ref_unet=ref_unet)
+                   num_reward=num_reward, process_group=process_group, ref_unet=ref_unet, latent_dtype=latent_dtype)
 
     # ------------------------------------------------------------------------------------------------------------
     # coefficients of transition j (host float32 scalars, the reference's operation order)
@@ -161,7 +253,7 @@ class PSOTrainer:
             t = self.timesteps[j].repeat(n)
             return pso_core.turbo_coef(self.sched.sigmas, self.sched.timesteps, t)
         t = self.timesteps[j].long().repeat(n)
-        return pso_core.dmd_coef(self.sched.alphas_cumprod, t, t - self.step_ratio)
+        return pso_core.dmd_coef(self.sched.alphas_cumprod, t, t - self.step_ratio, latent_dtype=self.latent_dtype)
 
     # ------------------------------------------------------------------------------------------------------------
     # SAMPLING: B prompts -> 2 trajectories each (independent x_T, T:572-608) -> buffer rows
@@ -181,6 +273,9 @@ class PSOTrainer:
         x = torch.randn(shape, device=dev, generator=generator, dtype=torch.float32)
         if self.mode == MODE_TURBO:
             x = x * float(self.sched.init_noise_sigma)
+        elif self.latent_dtype != torch.float32:  # x_T drawn in the latent dtype (DP/sdxl_dmd_with_logprob.py:91-101)
+            x = x.to(self.latent_dtype).float()
+        member = torch.arange(n_img, device=dev) % 2
         xs, ins, lps = [x], [], []
         for i in range(N):
             t = self.timesteps_dev[i].repeat(n_img)
@@ -195,9 +290,14 @@ class PSOTrainer:
                 if self.mode == MODE_TURBO:
                     noise = torch.randn(shape, device=dev, generator=generator)
                     x, lp = K.step_logprob(self.mode, x, eps, coef, noise=noise)
-                else:  # DMD2: one (1,C,H,W) draw shared across the batch (DP/distilled_...:123-126)
-                    noise = torch.randn((1,) + shape[1:], device=dev, generator=generator)
-                    x, lp = K.step_logprob(self.mode, x, eps, coef, noise=noise, noise_shared=True)
+                else:
+                    # DMD2: each trajectory is its own sdxl_dmd_pipeline_with_logprob call (D:585-618) whose step
+                    # re-noises with ONE (1,C,H,W) draw shared by that call's batch (DP/distilled_...:123-126): one
+                    # draw per pair member k, shared by the prompts, never by the two members of a pair
+                    noise = torch.randn((2,) + shape[1:], device=dev, generator=generator)
+                    if self.latent_dtype != torch.float32:
+                        noise = noise.to(self.latent_dtype).float()
+                    x, lp = K.step_logprob(self.mode, x, eps, coef, noise=noise[member].contiguous())
                 xs.append(x)
                 ins.append(model_in)
                 lps.append(lp)
@@ -302,6 +402,9 @@ class PSOTrainer:
         # accelerator.backward divides by gradient_accumulation_steps (accelerate accelerator.py:2840)
         deps = K.pair_loss_bwd(self.mode, mb.x, mb.x_next, eps_pol, mb.coef, pref, self.beta, self.clip_eps, ws,
                                grad_scale=count / self.gas_total)
+        if self.overlap_sync and self.auto_step and (self.n_micro + count) % self.gas_total == 0:
+            rt.unit_done = self.buckets.hook(rt)  # the window's last backward: overlap the gradient all-reduce
+            self.sync_armed = True
         u.backward_nhwc(deps, rt)
         self.loss_hist.append(loss)  # mean over the pass's pairs = mean of its micro-step losses
         self.n_micro += count
@@ -328,10 +431,15 @@ class PSOTrainer:
         if (sb.n_micro != self.gas_total or self.n_micro % self.gas_total or not self.auto_step
                 or (self.mode == MODE_TURBO and self.m > 1)):
             return self.train_epoch(sb, generator)
+        if getattr(self.unet, "full", None) is not None:
+            # full-UNet training: the optimizer step rebuilds the kernel-layout weight caches as new tensors
+            # (refresh_full -> prepare), which a captured graph would keep reading at their old addresses
+            return self.train_epoch(sb, generator)
         key = tuple((k, tuple(getattr(sb, k).shape)) for k in self._SB_TENSORS)
         g = getattr(self, "_graph", None)
         if g is None or self._graph_key != key:
             self._graph = None
+            self.overlap_sync = False  # no collective inside the captured region: the step's all-reduce is eager
             self._gsb = SimpleNamespace(n_micro=sb.n_micro, P=sb.P,
                                         **{k: getattr(sb, k).clone() for k in self._SB_TENSORS})
             _, st_grad, _ = trainable(self.unet)

@@ -158,7 +158,18 @@ class FullGradState:
     caches are rebuilt by UNet2DConditionModel.prepare())."""
 
     def __init__(self, unet):
-        params = [p for _, p in unet.named_parameters()]
+        # flat layout in the order the backward COMPLETES the parameters (UNet2DConditionModel.grad_units), so each
+        # all-reduce bucket of the overlapped gradient sync is one contiguous range that is final when issued
+        named = dict(unet.named_parameters())
+        order, seen = [], set()
+        for _, names in unet.grad_units():
+            for nm in names:
+                if nm in named and nm not in seen:
+                    order.append(nm)
+                    seen.add(nm)
+        order += [nm for nm in named if nm not in seen]
+        self.names = order
+        params = [named[nm] for nm in order]
         n = sum(p.numel() for p in params)
         dev = params[0].device
         self.params = params
@@ -173,6 +184,11 @@ class FullGradState:
             self._m[id(p)].copy_(p.data.float())
             off += k
         self.numel = n
+        self.offsets = {}
+        off = 0
+        for nm, p in zip(order, params):
+            self.offsets[nm] = (off, p.numel())
+            off += p.numel()
         self.trigger = torch.zeros(1, device=dev, requires_grad=True)  # autograd hook for UNet.forward (_UNetFn)
 
     def g(self, p):
@@ -894,6 +910,59 @@ class UNet2DConditionModel(nn.Module):
         self._adapters_enabled = True
         return self.lora
 
+    def grad_units(self):
+        """[(unit, [parameter names])] in the order backward_nhwc finishes them: conv_out / conv_norm_out, the up blocks
+        (upsampler, then per layer its attention and resnet, last layer first), the mid block, the down blocks, and
+        finally the embedding unit (conv_in, both embedding MLPs and every resnet's time_emb_proj, whose gradients
+        are formed from the accumulated time-embedding gradient after the sweep).  backward_nhwc calls
+        rt.unit_done(unit) at each of these points."""
+        units = [("conv_out", ["conv_out.weight", "conv_out.bias", "conv_norm_out.weight", "conv_norm_out.bias"])]
+        named = [n for n, _ in self.named_parameters()]
+
+        def under(prefix):
+            return [n for n in named if n.startswith(prefix + ".") and ".time_emb_proj." not in n]
+
+        for i in reversed(range(len(self.up_blocks))):
+            blk = self.up_blocks[i]
+            if hasattr(blk, "upsamplers"):
+                units.append((f"up_blocks.{i}.upsamplers.0", under(f"up_blocks.{i}.upsamplers.0")))
+            for j in reversed(range(len(blk.resnets))):
+                if hasattr(blk, "attentions"):
+                    units.append((f"up_blocks.{i}.attentions.{j}", under(f"up_blocks.{i}.attentions.{j}")))
+                units.append((f"up_blocks.{i}.resnets.{j}", under(f"up_blocks.{i}.resnets.{j}")))
+        for u in ("mid_block.resnets.1", "mid_block.attentions.0", "mid_block.resnets.0"):
+            units.append((u, under(u)))
+        for i in reversed(range(len(self.down_blocks))):
+            blk = self.down_blocks[i]
+            if hasattr(blk, "downsamplers"):
+                units.append((f"down_blocks.{i}.downsamplers.0", under(f"down_blocks.{i}.downsamplers.0")))
+            for j in reversed(range(len(blk.resnets))):
+                if hasattr(blk, "attentions"):
+                    units.append((f"down_blocks.{i}.attentions.{j}", under(f"down_blocks.{i}.attentions.{j}")))
+                units.append((f"down_blocks.{i}.resnets.{j}", under(f"down_blocks.{i}.resnets.{j}")))
+        units.append(("embed", [n for n in named if n.startswith(("conv_in.", "time_embedding.", "add_embedding."))
+                                or ".time_emb_proj." in n]))
+        return units
+
+    def grad_unit_ranges(self):
+        """[(unit, offset, numel)] of the trained flat gradient (LoRA bucket or full-UNet grad) in backward completion
+        order; every unit is one contiguous range (checked).  Units holding nothing trainable are dropped."""
+        out = []
+        if self.full is not None:
+            for unit, names in self.grad_units():
+                rs = sorted(self.full.offsets[n] for n in names if n in self.full.offsets)
+                if rs:
+                    out.append((unit, rs[0][0], sum(k for _, k in rs)))
+        elif self.lora is not None:
+            for unit, _ in self.grad_units():
+                rs = sorted((seg[0], seg[1] * seg[2]) for path, segs in self.lora.layout.items()
+                            if path.startswith(unit + ".") for seg in segs.values())
+                if rs:
+                    out.append((unit, rs[0][0], sum(k for _, k in rs)))
+        for (_, o, k), (_, o2, _) in zip(out, out[1:]):
+            assert o + k == o2, "gradient units must tile the flat buffer in completion order"
+        return out
+
     def enable_full_grads(self):
         """Train every UNet parameter (BASELINE C3 / C4; the reference has no such path, App. A #4): flat fp32
         master + grad over named_parameters; backward_nhwc then accumulates every weight gradient into self.full.grad
@@ -1105,22 +1174,30 @@ class UNet2DConditionModel(nn.Module):
                                   accumulate=True)
         else:
             dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True)
+        done = getattr(rt, "unit_done", None) or (lambda unit: None)  # overlapped gradient sync (trainer.GradBuckets)
+        done("conv_out")
         skip_grads = []
         for i in reversed(range(len(self.up_blocks))):
             blk = self.up_blocks[i]
             if hasattr(blk, "upsamplers"):
                 dh = blk.upsamplers[0].bwd(dh, rt)
+                done(f"up_blocks.{i}.upsamplers.0")
             for j in reversed(range(len(blk.resnets))):
                 if hasattr(blk, "attentions"):
                     dh = blk.attentions[j].bwd(dh, rt, f"up_blocks.{i}.attentions.{j}")
+                    done(f"up_blocks.{i}.attentions.{j}")
                 dhc = blk.resnets[j].bwd(dh, rt)
+                done(f"up_blocks.{i}.resnets.{j}")
                 c1 = rt.saved.pop()["c1"]
                 dh, ds = K.split_channels(dhc, c1)
                 skip_grads.append(ds)
         m = self.mid_block
         dh = m.resnets[1].bwd(dh, rt)
+        done("mid_block.resnets.1")
         dh = m.attentions[0].bwd(dh, rt, "mid_block.attentions.0")
+        done("mid_block.attentions.0")
         dh = m.resnets[0].bwd(dh, rt)
+        done("mid_block.resnets.0")
         # the up-block backward visits skips in forward-push order, so the down-block backward takes them from the end.
         # Below the first adapter-carrying attention (down_blocks.1.attentions.0) nothing has a trainable parameter and
         # the latent needs no gradient, so the backward stops there: down_blocks.0 (two 128^2 resnets + downsample),
@@ -1132,18 +1209,23 @@ class UNet2DConditionModel(nn.Module):
             if hasattr(blk, "downsamplers"):
                 dh = K.add(dh, skip_grads.pop())
                 dh = blk.downsamplers[0].bwd(dh, rt)
+                done(f"down_blocks.{i}.downsamplers.0")
             for j in reversed(range(len(blk.resnets))):
                 dh = K.add(dh, skip_grads.pop())
                 if (i, j) == (i0, j0):
                     blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}", need_dx=False)
+                    done(f"down_blocks.{i}.attentions.{j}")
                     break
                 if hasattr(blk, "attentions"):
                     dh = blk.attentions[j].bwd(dh, rt, f"down_blocks.{i}.attentions.{j}")
+                    done(f"down_blocks.{i}.attentions.{j}")
                 dh = blk.resnets[j].bwd(dh, rt)
+                done(f"down_blocks.{i}.resnets.{j}")
         if fg is not None:
             dh = K.add(dh, skip_grads.pop())  # conv_in output (the first skip)
             self._conv_in_dw(fg, dh, rt)
             self._embed_bwd(fg, rt)
+            done("embed")
         rt.saved.clear()  # activations of the never-differentiated prefix
         rt.side.join()  # LoRA weight gradients complete before anything reads lora.grad
         return None

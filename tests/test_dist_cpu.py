@@ -57,6 +57,81 @@ def test_gloo_world2_grad_sync_and_timing():
         assert t == 1.5
 
 
+def _bucket_worker(rank, world, port, q):
+    """GradBuckets on a fake 5-unit backward: buckets fire as their last unit completes, in completion order, and
+    the bucketed sum equals the flat all-reduce."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pairwise_sample_optimization_amd.trainer import GradBuckets
+        units = [("u0", 0, 300), ("u1", 300, 100), ("u2", 400, 500), ("u3", 900, 50), ("u4", 950, 74)]
+
+        class FakeUNet:
+            def grad_unit_ranges(self):
+                return units
+
+        torch.manual_seed(10 + rank)
+        flat = torch.randn(1024)
+        expect = flat.clone()
+        dist.all_reduce(expect)
+        gb = GradBuckets(FakeUNet(), flat, bucket_mb=400 * 4 / 1e6)   # 400-element buckets
+        spans = [(o, n) for o, n, _ in gb.buckets]
+        rt = type("RT", (), {})()
+        done = gb.hook(rt)
+        issued = []
+        for u, _, _ in units:
+            done(u)
+            issued.append(sum(w is not None for w in gb.works))
+        scale = gb.finish()
+        q.put((rank, spans, issued, torch.equal(flat, expect), scale))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_bucketed_overlap_sync():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    for rank, spans, issued, equal, scale in res:
+        assert spans == [(0, 400), (400, 500), (900, 124)]   # contiguous, completion-ordered buckets
+        assert issued == [0, 1, 2, 2, 3]                      # each fires with its last unit, not at the end
+        assert equal and scale == 0.5
+
+
+@pytest.mark.parametrize("full", [False, True])
+def test_grad_units_tile_the_flat_gradient(full):
+    """The backward's unit order (UNet2DConditionModel.grad_units) tiles the trained flat gradient contiguously --
+    the LoRA layout (reverse forward order of blocks) and the full-UNet layout (ordered by grad_units) -- so every
+    all-reduce bucket is final when it is issued.  Host-only (CPU tensors, no kernel runs)."""
+    from types import SimpleNamespace
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    unet = UNet2DConditionModel(UNetConfig.tiny(16))
+    if full:
+        fg = unet.enable_full_grads()
+        n = fg.numel
+        assert n == sum(p.numel() for p in unet.parameters())
+    else:
+        st = unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+        n = st.numel
+    ranges = unet.grad_unit_ranges()
+    assert ranges[0][1] == 0 and sum(k for _, _, k in ranges) == n
+    names = [u for u, _, _ in ranges]
+    assert len(names) == len(set(names))
+    if full:
+        assert names[0] == "conv_out" and names[-1] == "embed"
+    else:
+        assert names[0].startswith("up_blocks.1.attentions") and names[-1] == "down_blocks.1.attentions.0"
+
+
 def test_single_process_sync_is_identity():
     from pairwise_sample_optimization_amd.trainer import allreduce_grads
     g = torch.ones(3)

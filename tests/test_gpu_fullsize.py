@@ -1,0 +1,266 @@
+"""Parity at the BENCH configurations' full size (SDXL UNet at 1024^2 = 128x128 latents) -- the shapes the bench
+actually runs (256x256 / 128x160 tiles, split-K paths, the 16384-pixel-row T2 / UP2 gathers, the 16-image paired
+pass), against the plain-torch fp32 oracle (oracle/sdxl_ref.py) run on the GPU:
+
+  * C2 (BASELINE configs[1]): the turbo accumulation window of bench.py's default (P = 2 pairs, gas 2, N = 2, LoRA
+    r = 32) as ONE paired pass of 16 images -- eps of every policy / reference image, the window loss and every LoRA
+    gradient (T:775-857 per micro-step, summed over the window as accelerate's accumulation does);
+  * C3 (configs[2]): the DMD2 full-UNet window (N = 4, T = 3, P = 1) -- loss and the gradient of all 1,680 UNet
+    parameter tensors against a frozen reference UNet;
+  * the VAE decoder at 1024^2 (DP/sdxl_turbo_with_logprob.py:154-155).
+
+Loss bar: the HIP path must sit within the reference's OWN bf16 noise -- |mine - fp32| <= 1.5 |torch_bf16 - fp32| +
+2e-3 (relative), where torch_bf16 is the same oracle micro-step with the UNet cast to bf16 (T:299-321) under
+torch.autocast(bfloat16) (accelerate's mixed_precision="bf16"); the LoRA / full gradients are held to the same form
+against that run's gradients.  north_star's 1e-3 loss bar is a property of the fp32 eps path (the loss kernel alone:
+5e-5 against the reference's own functions, golden).
+The oracle runs image by image (the pair loss couples images only through the scalar log-probs), so its fp32
+autograd graph holds one 1024^2 image at a time."""
+import math
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-30)).item()
+
+
+def _lp(mode, x, eps, prev, c):
+    """Step log-prob of one image in fp32 torch (DP/turbo_inference_with_logprob.py:69-114 for mode 0,
+    DP/distilled_inference_with_logprob.py:84-135 for DMD modes), differentiable in eps.  c = the kernel's coef row."""
+    if mode == 0:
+        sig, su, dt = c[0], c[1], c[2]
+        pred = x - sig * eps
+        mean = x + (x - pred) / sig * dt
+        std = su
+    else:
+        x0 = (x - c[1] * eps) / c[0]
+        mean = c[2] * x0
+        std = c[3]
+    lp = -((prev - mean) ** 2) / (2 * std ** 2) - torch.log(std) - LOG_SQRT_2PI
+    return lp.mean()
+
+
+def _pair_loss(lp_pol, lp_ref, pref, beta=50.0, eps=0.1):
+    """T:844-850 on [P, 2] log-probs."""
+    ratio = torch.clamp(torch.exp(lp_pol - lp_ref), 1 - eps, 1 + eps)
+    return -torch.log(torch.sigmoid(beta * torch.log(ratio[:, 0]) * pref[:, 0] +
+                                    beta * torch.log(ratio[:, 1]) * pref[:, 1])).mean()
+
+
+def _oracle_window(unet_sd, mb, tr, cfg, lora_leaf=None, param_leaf=None, ref_sd=None, grads16=None):
+    """fp32 oracle of one accumulation window held in mb (count micro-steps of P pairs, image 2p + k, NHWC buffers).
+    Returns (eps_pol [n], eps_ref [n], window loss (mean of micro-step losses), torch-bf16 window loss); the
+    gradients of the summed sum_s loss_s / gas_total are accumulated into lora_leaf / param_leaf .grad, and -- when
+    grads16 is a dict -- the torch-bf16 run's gradients of the same leaves into grads16."""
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd import kernels as K
+    ocfg = dict(time_proj_dim=cfg.time_proj_dim, addition_time_embed_dim=cfg.addition_time_embed_dim)
+    n = mb.unet_in.shape[0]
+    P = tr.P
+    count = n // (2 * P)
+    x_in = K.nhwc_to_nchw(mb.unet_in).float()
+    xs, xp = mb.x.permute(0, 3, 1, 2), mb.x_next.permute(0, 3, 1, 2)
+    pol_w = param_leaf if param_leaf is not None else unet_sd
+    rsd = ref_sd if ref_sd is not None else unet_sd
+
+    def fwd(i, w, lora):
+        return sdxl_ref.unet_forward(w, x_in[i:i + 1], mb.t[i:i + 1], mb.enc[i:i + 1].float(),
+                                     mb.pooled[i:i + 1].float(), mb.tid[i:i + 1], lora=lora, cfg=ocfg)
+
+    bf = lambda d: {k: v.detach().bfloat16() for k, v in d.items()}  # the UNet cast to weight_dtype (T:299-321)
+    with torch.no_grad():
+        lora_d = {k: v.detach() for k, v in lora_leaf.items()} if lora_leaf is not None else None
+        pw_d = {k: v.detach() for k, v in pol_w.items()}
+        ep = torch.cat([fwd(i, pw_d, lora_d) for i in range(n)])
+        er = torch.cat([fwd(i, rsd, None) for i in range(n)])
+        print("  oracle fp32 forwards done", flush=True)
+        pw16, rsd16 = bf(pw_d), bf(rsd)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ep16 = torch.cat([fwd(i, pw16, lora_d).float() for i in range(n)])
+            er16 = torch.cat([fwd(i, rsd16, None).float() for i in range(n)])
+        print("  oracle bf16-autocast forwards done", flush=True)
+    # the reference feeds the step functions fp32 eps holding bf16 values (accelerate convert_outputs_to_fp32)
+    epb, erb = ep.bfloat16().float(), er.bfloat16().float()
+    pref = K.preference(mb.rewards, 0 if tr.mode == 0 else 1)            # [count*P, 2]
+    c = mb.coef
+    eps_leaf = epb.clone().requires_grad_(True)
+    lpp = torch.stack([_lp(tr.mode, xs[i], eps_leaf[i], xp[i], c[i]) for i in range(n)]).view(count * P, 2)
+    lpr = torch.stack([_lp(tr.mode, xs[i], erb[i], xp[i], c[i]) for i in range(n)]).view(count * P, 2)
+    losses = torch.stack([_pair_loss(lpp[s * P:(s + 1) * P], lpr[s * P:(s + 1) * P], pref[s * P:(s + 1) * P])
+                          for s in range(count)])
+    (losses.sum() / tr.gas_total).backward()                            # accelerate: loss / gas per micro-step
+    e16_leaf = ep16.bfloat16().float().clone().requires_grad_(True)
+    l16 = torch.stack([_lp(tr.mode, xs[i], e16_leaf[i], xp[i], c[i]) for i in range(n)]).view(count * P, 2)
+    r16 = torch.stack([_lp(tr.mode, xs[i], er16[i].bfloat16().float(), xp[i], c[i]) for i in range(n)])
+    r16 = r16.view(count * P, 2)
+    losses16 = torch.stack([_pair_loss(l16[s * P:(s + 1) * P], r16[s * P:(s + 1) * P], pref[s * P:(s + 1) * P])
+                            for s in range(count)])
+    (losses16.sum() / tr.gas_total).backward()
+    loss16 = losses16.mean().item()
+    if grads16 is not None:  # the bf16 run's parameter gradients, image by image
+        # fp32 leaves holding the bf16 values: autocast casts them for every conv / linear exactly as it does the
+        # bf16 module weights, and the norms run in fp32 either way, so the activations match the bf16-weight run
+        leaves = lora_leaf if lora_leaf is not None else param_leaf
+        lw16 = {k: v.detach().clone().requires_grad_(True) for k, v in leaves.items()}
+        for i in range(n):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = fwd(i, lw16, None) if lora_leaf is None else fwd(i, pw16, lw16)
+            (out.float() * e16_leaf.grad[i:i + 1]).sum().backward()
+            del out
+            print(f"  torch-bf16 backward image {i + 1}/{n}", flush=True)
+        grads16.update({k: v.grad for k, v in lw16.items()})
+    # parameter gradients image by image: d(window loss)/d eps_i, pushed through one fp32 UNet graph at a time
+    g_eps = eps_leaf.grad
+    for i in range(n):
+        out = fwd(i, pol_w, lora_leaf)
+        (out * g_eps[i:i + 1]).sum().backward()
+        del out
+        print(f"  oracle backward image {i + 1}/{n}", flush=True)  # progress (the fp32 oracle takes minutes)
+    return ep, er, losses.mean().item(), loss16
+
+
+def _window(tr, buf, g):
+    sb = tr.shuffle(buf, generator=g)
+    assert sb.n_micro == tr.gas_total
+    return tr.micro_batch(sb, 0, sb.n_micro)
+
+
+def test_c2_turbo_lora_window_at_1024(cuda):
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    h, P, gas, N, r = 128, 2, 2, 2, 32
+    cfg = UNetConfig.sdxl(h)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(SimpleNamespace(r=r, lora_alpha=r))
+    unet.lora.init_gaussian(seed=0, b_std=2e-3)  # LoRA effect a few % of eps: the loss is not log 2
+    unet.prepare()
+    tr = PSOTrainer(unet, mode="turbo", num_steps=N, gradient_accumulation_steps=gas, train_batch_size=P)
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(1000)
+    Bp = P * gas
+    enc = torch.randn(Bp, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(Bp, 1280, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(1024, 0, cuda).repeat(Bp, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g,
+                          reward_fn=lambda img: torch.rand(img.shape[0], device=cuda, generator=g))
+    mb = _window(tr, buf, g)
+    n = mb.unet_in.shape[0]
+    assert n == 8  # the bench's window: 4 pairs -> 8 policy + 8 reference images in ONE paired pass
+    with torch.no_grad():
+        eps_both, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False, paired_ref=True)
+    from pairwise_sample_optimization_amd import kernels as K
+    e_pol, e_ref = K.nhwc_to_nchw(eps_both[:n]), K.nhwc_to_nchw(eps_both[n:])
+    st = unet.lora
+    st.grad.zero_()
+    mine_loss = tr.micro_step(mb).item()
+    mine = {k: v.clone() for k, v in st.grad_dict_peft().items()}
+    sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
+    leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
+    g16 = {}
+    ep, er, ref_loss, loss16 = _oracle_window(sd, mb, tr, cfg, lora_leaf=leaf, grads16=g16)
+    rp, rr = _rel(e_pol, ep), _rel(e_ref, er)
+    rel = abs(mine_loss - ref_loss) / abs(ref_loss)
+    rel16 = abs(loss16 - ref_loss) / abs(ref_loss)
+    den = sum((v.grad ** 2).sum().item() for v in leaf.values())
+    grel = (sum(((mine[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    print(f"C2 @1024: eps rel pol {rp:.2e} ref {rr:.2e}; loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} "
+          f"torch-bf16 {loss16:.6f} rel(mine) {rel:.2e} rel(torch-bf16) {rel16:.2e}; LoRA grad rel mine {grel:.3e} "
+          f"torch-bf16 {grel16:.3e} over {len(leaf)} tensors")
+    assert rp < 3e-2 and rr < 3e-2
+    assert rel <= 1.5 * rel16 + 2e-3
+    assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
+
+
+def test_c3_dmd_full_unet_window_at_1024(cuda):
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    h, P, gas, N = 128, 1, 1, 4
+    cfg = UNetConfig.sdxl(h)
+
+    def make():
+        with torch.device(cuda):
+            u = UNet2DConditionModel(cfg)
+        u.init_weights(0)
+        return u
+
+    unet, ref_unet = make(), make()
+    fg = unet.enable_full_grads()
+    ref_unet.prepare()
+    unet.prepare()
+    # policy != reference (after a few updates in a real run): perturb the policy's bf16 weights slightly
+    with torch.no_grad():
+        gp = torch.Generator(device="cuda").manual_seed(7)
+        for p in unet.parameters():
+            p.add_((torch.randn(p.shape, device=cuda, generator=gp) * 2e-3 * p.float().abs().mean()).bfloat16())
+        fg.master.copy_(torch.cat([p.detach().float().reshape(-1) for p in fg.params]))
+    unet.prepare()
+    tr = PSOTrainer(unet, mode="dmd", num_steps=N, gradient_accumulation_steps=gas, train_batch_size=P,
+                    ref_unet=ref_unet)
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(2000)
+    enc = torch.randn(P, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(P, 1280, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(1024, 0, cuda).repeat(P, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g,
+                          reward_fn=lambda img: torch.rand(img.shape[0], device=cuda, generator=g))
+    mb = _window(tr, buf, g)
+    assert mb.unet_in.shape[0] == 6  # T = 3 micro-steps x 1 pair x 2 members
+    fg.grad.zero_()
+    mine_loss = tr.micro_step(mb).item()
+    mine = {unet._unmap_key(nm): fg.g(p) for nm, p in unet.named_parameters()}
+    sd_ref = sdxl_ref.sd_to(ref_unet.state_dict(), cuda)
+    leaf = {k: v.clone().requires_grad_(True) for k, v in sdxl_ref.sd_to(unet.state_dict(), cuda).items()}
+    g16 = {}
+    _, _, ref_loss, loss16 = _oracle_window(None, mb, tr, cfg, param_leaf=leaf, ref_sd=sd_ref, grads16=g16)
+    rel = abs(mine_loss - ref_loss) / abs(ref_loss)
+    rel16 = abs(loss16 - ref_loss) / abs(ref_loss)
+    num = den = 0.0
+    gmax = max(v.grad.norm().item() for v in leaf.values() if v.grad is not None)
+    worst = []
+    for k, v in leaf.items():
+        assert v.grad is not None, k
+        num += (mine[k] - v.grad).norm().item() ** 2
+        den += v.grad.norm().item() ** 2
+        if v.grad.norm().item() > 1e-3 * gmax:
+            worst.append((_rel(mine[k], v.grad), k))
+    grel = (num / den) ** 0.5
+    grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    worst.sort(reverse=True)
+    print(f"C3 @1024: loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} torch-bf16 {loss16:.6f} rel(mine) {rel:.2e} "
+          f"rel(torch-bf16) {rel16:.2e}; full grad rel mine {grel:.3e} torch-bf16 {grel16:.3e} over {len(leaf)} "
+          f"tensors; worst {worst[:3]}")
+    assert len(leaf) == len(mine) == 1680
+    assert rel <= 1.5 * rel16 + 2e-3
+    assert grel <= 1.5 * grel16 + 1e-2 and grel < 5e-2
+    assert all(r_ < 0.2 for r_, _ in worst)
+
+
+def test_vae_decode_at_1024(cuda):
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd.vae import AutoencoderKL, VAEConfig
+    with torch.device(cuda):
+        vae = AutoencoderKL(VAEConfig())
+    vae.init_weights(0)
+    z = torch.randn(2, 4, 128, 128, device=cuda, generator=torch.Generator(device="cuda").manual_seed(3))
+    z = z.bfloat16().float()
+    img = vae.decode(z / vae.config.scaling_factor, return_dict=False)[0]
+    sd = sdxl_ref.sd_to(vae.state_dict(), cuda)
+    with torch.no_grad():
+        ref = torch.cat([sdxl_ref.vae_decode(sd, (z[i:i + 1] / vae.config.scaling_factor).bfloat16().float())
+                         for i in range(2)])
+    rel = _rel(img, ref)
+    print(f"vae decode @1024^2: rel err {rel:.3e}")
+    assert img.shape == (2, 3, 1024, 1024)
+    assert rel < 3e-2

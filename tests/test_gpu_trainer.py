@@ -69,11 +69,13 @@ def test_micro_step_loss_and_grad_vs_fp32_reference(cuda, P):
     ref_loss = -torch.log(torch.sigmoid(50 * torch.log(ratio[:, 0]) * pref[:, 0] +
                                         50 * torch.log(ratio[:, 1]) * pref[:, 1])).mean()
     (ref_loss / tr.gas_total).backward()  # accelerator.backward divides by gradient_accumulation_steps = gas*T
-    # the reference's own numerics: the same micro-step under bf16 autocast (accelerate mixed_precision="bf16")
+    # the reference's own numerics: the UNet cast to weight_dtype = bf16 (T:299-321) run under accelerate's bf16
+    # autocast -- bf16 hidden states and residual stream, fp32 norms / softmax
+    sd16 = sdxl_ref.sd_to(unet.state_dict(), cuda, torch.bfloat16)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-        ep16 = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid,
+        ep16 = sdxl_ref.unet_forward(sd16, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid,
                                      lora={k: v.detach() for k, v in leaf.items()}, cfg=ocfg).float()
-        er16 = sdxl_ref.unet_forward(sd, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid, lora=None,
+        er16 = sdxl_ref.unet_forward(sd16, x_in, mb.t, mb.enc.float(), mb.pooled.float(), mb.tid, lora=None,
                                      cfg=ocfg).float()
     with torch.no_grad():
         d16 = (_ref_turbo_lp(xs, ep16, xp, sig, su, dt) - _ref_turbo_lp(xs, er16, xp, sig, su, dt)).view(P, 2)
@@ -88,9 +90,10 @@ def test_micro_step_loss_and_grad_vs_fp32_reference(cuda, P):
     print(f"P={P}: loss mine={mine_loss:.6f} fp32-ref={ref_loss.item():.6f} torch-bf16={loss16:.6f} "
           f"rel(mine)={rel:.2e} rel(torch-bf16)={rel16:.2e}; grad rel={grel:.3e}")
     # Both bf16 paths see eps_pol - eps_ref (the LoRA effect) through ~1% bf16 activation noise, which beta=50
-    # amplifies into the loss (torch's own bf16 run lands 1e-2 away from fp32 on some seeds).  Bar: 2e-2 here;
-    # loss-kernel parity on identical eps is 1e-5 (test_gpu_pso_loss).
-    assert rel < 2e-2
+    # amplifies into the loss (torch's own bf16 run lands 1e-2 away from fp32 on some seeds).  Bar: the HIP path
+    # within the reference's own bf16 noise, |mine - fp32| <= 1.5 |torch_bf16 - fp32| + 2e-3 (relative); the loss
+    # kernel alone on identical eps is within 5e-5 of the reference (test_gpu_pso_loss, golden).
+    assert rel <= 1.5 * rel16 + 2e-3
     if den > 0:
         assert grel < 1e-1
 
@@ -312,3 +315,69 @@ def test_full_unet_micro_step_vs_fp32_reference(cuda):
           f"grad rel over {len(leaf)} tensors={grel:.3e}")
     assert rel < 2e-2
     assert grel < 1e-1
+
+
+def test_dmd_sampling_noise_per_pair_member(cuda, monkeypatch):
+    """DMD2 re-noising: each trajectory of a pair is its own pipeline call (D:585-618) whose step draws ONE (1,C,H,W)
+    noise shared by that call's batch (DP/distilled_inference_with_logprob.py:123-126) -- so the two members of a
+    pair get different draws while images with the same member index share one."""
+    from pairwise_sample_optimization_amd import trainer as T_
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+    tr = PSOTrainer(unet, mode="dmd", num_steps=3, train_batch_size=1)
+    seen = []
+    real = T_.K.step_logprob
+
+    def spy(mode, x, eps, coef, prev=None, noise=None, noise_shared=False):
+        if noise is not None and noise.abs().sum() > 0:
+            seen.append((noise.clone(), noise_shared))
+        return real(mode, x, eps, coef, prev=prev, noise=noise, noise_shared=noise_shared)
+
+    monkeypatch.setattr(T_.K, "step_logprob", spy)
+    B = 3
+    g = torch.Generator(device="cuda").manual_seed(4)
+    enc = torch.randn(B, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(B, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    tr.sample_pairs(enc, pooled, compute_time_ids(128, 0, cuda).repeat(B, 1), 16, generator=g)
+    assert len(seen) == 2  # N - 1 stochastic transitions
+    for noise, shared in seen:
+        n = noise if not shared else noise.expand(2 * B, *noise.shape[1:])
+        assert not torch.equal(n[0], n[1])                       # the two members of a pair differ
+        for b in range(1, B):
+            assert torch.equal(n[2 * b], n[0]) and torch.equal(n[2 * b + 1], n[1])  # shared across prompts
+
+
+def test_graph_epoch_falls_back_to_eager_for_full_unet(cuda):
+    """train_epoch_graph must not capture a full-UNet epoch: its optimizer step rebuilds the kernel-layout weight
+    caches as new tensors that a replayed graph would not see.  Two epochs run eagerly and train."""
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+
+    def make():
+        with torch.device(cuda):
+            u = UNet2DConditionModel(cfg)
+        u.init_weights(0)
+        return u
+
+    unet, ref = make(), make()
+    unet.enable_full_grads()
+    ref.prepare()
+    tr = PSOTrainer(unet, mode="turbo", num_steps=2, train_batch_size=1, ref_unet=ref, lr=1e-4)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    enc = torch.randn(1, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(1, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    buf = tr.sample_pairs(enc, pooled, compute_time_ids(128, 0, cuda), 16, generator=g,
+                          reward_fn=lambda x: torch.rand(x.shape[0], device=cuda, generator=g))
+    w0 = unet.conv_out.weight.detach().clone()
+    for _ in range(2):
+        tr.train_epoch_graph(tr.shuffle(buf, generator=g))
+    torch.cuda.synchronize()
+    assert getattr(tr, "_graph", None) is None and tr.opt_step == 2
+    assert torch.isfinite(torch.stack(tr.loss_hist)).all()
+    assert not torch.equal(unet.conv_out.weight, w0)
