@@ -128,6 +128,8 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
  * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
  * 6 = 64x128 (4 waves), 7 = 128x256 (8 waves), 8 = 128x128 (8 waves). */
 void pso_gemm_set_variant(int v);
+/* Benchmark knob of the 8-phase 256x256 kernel: 1 = keep the accumulators live but store nothing (main-loop cost). */
+void pso_gemm8p_skip_epilogue(int on);
 /* Benchmark knob: split count of pso_gemm_tn over the reduction rows (0 = automatic). */
 void pso_gemm_tn_set_split(int ks);
 /* benchmark knob: attention forward tile (0 = auto, 2 = 128 / 4 = 256 queries per workgroup) */

@@ -45,6 +45,7 @@ SIGNATURES = {
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
+    "pso_gemm8p_skip_epilogue": (None, [ci]),
     "pso_gemm_tn_set_split": (None, [ci]),
     "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),

@@ -746,11 +746,12 @@ int pso_gemm_skinny_nt(int M, int N, int K, const void* A, long lda, const void*
 int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long ldu, int R, int group_c, float alpha,
                      float* out, long ldo, int out_jc, hipStream_t st);
 
-// 8-phase 256x256 kernel (gemm8p.hip): dense A . W^T (+ bias) -> bf16, and the GEGLU-epilogue form
-int pso_gemm8p(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias, void* out,
-               long ldo, int group_m, hipStream_t st);
-int pso_gemm8p_geglu(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
-                     void* out, long ldo, void* out_pre, long ld_pre, int pre_rows, int group_m, hipStream_t st);
+// 8-phase 256x256 kernel (gemm8p.hip): epi 0 dense (+ LoRA K-tail, bias, alpha, residual), 1 GEGLU, 2 GEGLU backward
+int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2,
+                   long lda2, int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha,
+                   const void* bias, const void* resid, long ldr, void* out, long ldo, void* out2, long ldo2,
+                   int pre_rows, const void* aux, long ldaux, int group_m, hipStream_t st);
+static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
@@ -795,13 +796,19 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if (ks < 1) ks = 1;
     return launch<64, 64>(g, st, (int)ks);
   }
-  // 8-phase 256x256 (variant 30 forces it where it applies): dense bf16 out, optional bias, K % 128 == 0
-  const bool ok8 = !g.conv.mode && !g.a2 && !g.rowbias && !g.resid && g.out_dtype == PSO_BF16 && !g.accumulate &&
-                   g.alpha == 1.f && (g.N % 256) == 0 && (g.K1 % 128) == 0 && g.vec_ok && al16(g.a1) && al16(g.b1) &&
-                   (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 && (long)g.M * g.lda1 < (1L << 30) &&
-                   (long)g.N * g.ldb1 < (1L << 30);
-  if (gv == 30 && ok8)
-    return pso_gemm8p(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.bias, g.out, g.ldo, g.group_m, st);
+  // 8-phase 256x256 (gemm8p.hip) for every dense bf16 GEMM with N % 256 == 0 and enough tiles to fill the chip:
+  // LDS-staged 16-B epilogue, LoRA K-tail, bias / alpha / residual.  Variant 31 keeps the 2-phase kernels (A/B knob).
+  const bool ok8 = !g.conv.mode && !g.rowbias && g.out_dtype == PSO_BF16 && !g.accumulate && (g.N % 256) == 0 &&
+                   (g.K1 % 64) == 0 && al16(g.a1) && al16(g.b1) && (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 &&
+                   al16(g.out) && (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
+                   (!g.bias || al8(g.bias)) && fits30(g.M, g.lda1) && fits30(g.N, g.ldb1) &&
+                   (!g.a2 || ((g.tail_group_n == 0 || (g.tail_group_n % 256) == 0) && fits30(g.tail_m, g.lda2) &&
+                              fits30(g.N, g.ldb2)));
+  const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
+  if (ok8 && gv != 31 && (gv == 30 || (gv == 0 && t256 >= 256)))
+    return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
+                          g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
+                          g.group_m, st);
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
@@ -1040,11 +1047,11 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   g.tail_m = (pre_rows > 0 && pre_rows < M) ? pre_rows : M;
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
-  // variant 32: the 8-phase kernel (gemm8p.hip; K % 128 == 0).  Measured equal on the UNet GEGLU shapes (16384 x
-  // 10240 x 1280: 877 vs 879 TF/s; 65536 x 5120 x 640: 701 vs 697), so the 2-phase 256x256 kernel stays the default.
-  if (g_gemm_variant == 32 && (K % 128) == 0 && (long)M * lda < (1L << 30) && (long)N * ldw < (1L << 30))
-    return pso_gemm8p_geglu(M, N, K, a, lda, w, ldw, bias, out, ldo, out_pre, ld_pre, g.tail_m, g.group_m,
-                            (hipStream_t)stream);
+  // the 8-phase kernel with the LDS-staged epilogue (gemm8p.hip): 16384 x 10240 x 1280 1023 vs 801 TF/s,
+  // 65536 x 5120 x 640 814 vs 640 (tools/gemm_bench.py, one box); variant 31 keeps the 2-phase 256x256 kernel
+  if (g_gemm_variant != 31 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw))
+    return pso_gemm8p_run(1, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, bias, nullptr, 0, out, ldo,
+                          out_pre, ld_pre, g.tail_m, nullptr, 0, g.group_m, (hipStream_t)stream);
   // tile A/B knobs (64-column wave tiles are what the interleaved epilogue needs)
   if (g_gemm_variant == 33) return launch<128, 128, 2, 2, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
   if (g_gemm_variant == 34) return launch<128, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
@@ -1070,6 +1077,10 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   const hipStream_t st = (hipStream_t)stream;
+  if (g_gemm_variant != 31 && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw) &&
+      (long)((M + 255) / 256) * (N / 256) >= 128)
+    return pso_gemm8p_run(2, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, nullptr, nullptr, 0, out,
+                          ldo, nullptr, 0, 0, pre, ld_pre, g.group_m, st);
   const long t160 = (long)((M + 127) / 128) * ((N + 159) / 160);
   if ((N % 160) == 0 && t160 >= 256) return launch<128, 160, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);
   return launch<64, 64, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);

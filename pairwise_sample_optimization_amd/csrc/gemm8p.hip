@@ -1,10 +1,13 @@
 // 256 x 256 bf16 MFMA GEMM with an 8-phase software pipeline for gfx950, fp32 accumulate.
 //
-//   out = EPI(A[M][K] . W[N][K]^T + bias)      EPI_NONE: bf16 out[M][N];  EPI_GEGLU: out[M][N/2] = h * gelu(gate)
-//   (+ optional interleaved pre-activation rows, see gemm.hip GemmArgs) -- dense operands, no K-tail.
+//   acc = A[M][K1] . W[N][K1]^T (+ A2[M][K2] . W2[N][K2]^T, the LoRA up-projection as a K-tail on rows < tail_m)
+//   EPI_NONE:      out[M][N]   = bf16(alpha * acc + bias) (+ resid, added to the rounded projection)
+//   EPI_GEGLU:     out[M][N/2] = h * gelu(gate) of the interleaved [h 32 | gate 32] columns (+ pre-activation rows)
+//   EPI_GEGLU_BWD: acc = dout [M][N]; out[M][2N] = interleaved [dout * gelu(g) | dout * h * gelu'(g)] from aux = pre
 //
-// Serves the widest GEMMs of the UNet step: the GEGLU projection ff.net.0.proj (16384 x 10240 x 1280 and
-// 65536 x 5120 x 640 in the paired pass; replaces diffusers GEGLU's nn.Linear + gelu).
+// Serves the widest GEMMs of the UNet step (N % 256 == 0): the GEGLU projection ff.net.0.proj (16384 x 10240 x 1280
+// and 65536 x 5120 x 640 in the paired pass; diffusers GEGLU's nn.Linear + gelu), its backward through
+// ff.net.2 (GEGLU_BWD) and the fused self-attention q/k/v projection with its LoRA tail (N = 3C = 3840).
 //
 // Structure (one workgroup = 8 waves = a 256 x 256 output tile, 1 per CU):
 //   * The K-tile (BK = 64) is split into four half-tile images A0 A1 (rows 0-127 / 128-255) and B0 B1 (columns),
@@ -25,6 +28,7 @@
 
 #define EPI8_NONE 0
 #define EPI8_GEGLU 1
+#define EPI8_GEGLU_BWD 2
 
 typedef __attribute__((address_space(3))) void lds8_void;
 
@@ -32,10 +36,17 @@ struct Gemm8Args {
   const bf16_t* a; long lda;
   const bf16_t* w; long ldw;
   int M, N, K;
+  const bf16_t* a2; long lda2; int K2;  // LoRA K-tail (a2 null: none); a2 has tail_m rows
+  const bf16_t* w2; long ldw2;
+  int tail_m, tail_group_n;              // tail_group_n > 0: column group j takes a2 columns [j*K2, (j+1)*K2)
+  float alpha;
   const bf16_t* bias;
+  const bf16_t* resid; long ldr;
   void* out; long ldo;
   void* out2; long ldo2; int pre_rows;  // EPI_GEGLU: interleaved pre-activation of rows < pre_rows (optional)
+  const bf16_t* aux; long ldaux;        // EPI_GEGLU_BWD: interleaved pre-activation [M][2N]
   int group_m;
+  int skip_epi;  // benchmark knob: accumulators kept live, nothing stored (main-loop time alone)
 };
 
 namespace {
@@ -71,7 +82,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     bn = in / gsz;
   }
   const int m0 = bm * 256, n0 = bn * 256;
-  const int nt = g.K / 64;  // even (host-checked)
+  const int nt1 = g.K / 64;  // K % 64 == 0 (host-checked)
+  // the LoRA K-tail: tiles made only of rows >= tail_m (the reference half of a paired pass) skip it (zero there)
+  const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + 63) / 64 : 0;
+  const int nt = (nt1 + nt2 + 1) & ~1;  // the 8-phase loop consumes K-tiles in pairs: an odd count gets a zero tile
 
   // staging: wave w fills pieces 2w, 2w+1 (8 rows x 128 B each) of every half-tile image; the XOR swizzle is applied
   // on the source chunk (lane i lands at byte 16 i of its piece).  Rows past M are clamped (never stored).  The loads
@@ -91,17 +105,43 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     }
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.a2 ? g.a2 : g.a), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.w2 ? g.w2 : g.w), (short)0, 0x7fffffff, 0x00020000);
+  // a byte offset past the buffer range: the raw buffer load returns zeros (padding of the K-tail / zero tile)
+  constexpr unsigned OOB = 0x80000000u;
+  const long a2_col = g.tail_group_n > 0 ? (long)(n0 / g.tail_group_n) * g.K2 : 0;
   // image index = buf * 4 + {A0 0, A1 1, B0 2, B1 3}
   auto stage = [&](int kt, int img) {
     const int half = img & 3;
     bf16_t* dst = l8 + img * HT + wave * 2 * 8 * 64;
-    const unsigned k0 = (unsigned)kt * 128u;  // bytes
-    if (half < 2) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, aoff[half][0] + k0, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, aoff[half][1] + k0, 0, 0, 0);
-    } else {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, woff[half - 2][0] + k0, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, woff[half - 2][1] + k0, 0, 0, 0);
+    if (kt < nt1) {
+      const unsigned k0 = (unsigned)kt * 128u;  // bytes
+      if (half < 2) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, aoff[half][0] + k0, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, aoff[half][1] + k0, 0, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, woff[half - 2][0] + k0, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, woff[half - 2][1] + k0, 0, 0,
+                                                 0);
+      }
+    } else {  // LoRA K-tail (one or two K-tiles per output tile) or the zero pad tile
+      const int kc = (kt - nt1) * 64 + (pch ^ prow) * 8;  // this lane's 8 columns of the tail
+      const bool kin = kt < nt1 + nt2 && kc < g.K2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int R = (half & 1) * 128 + (wave * 2 + i) * 8 + prow;
+        unsigned off;
+        if (half < 2) {
+          const int m = m0 + R;
+          off = (kin && m < g.tail_m) ? (unsigned)(((long)m * g.lda2 + a2_col + kc) * 2) : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rA2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
+        } else {
+          off = kin ? (unsigned)(((long)(n0 + R) * g.ldw2 + kc) * 2) : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
+        }
+      }
     }
   };
 
@@ -199,75 +239,130 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #undef PHASE
 
   // ---- epilogue: lane holds out[m = m0 + 128 ha + 32 wr + 16 i + fr][n = n0 + 128 hb + 64 wc + 16 j + 4 fk + r] ----
-  if constexpr (EPI == EPI8_GEGLU) {
-    // columns 64 wc .. +64 of each B half = one interleaved group: j = 0,1 hold h, j = 2,3 the matching gate.
-    // B half outermost: only its 16 bias values are live beside the accumulators.
+  if (g.skip_epi) {
 #pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-      const int ng = n0 + hb * 128 + wc * 64;
-      float bh[2][4], bg[2][4];
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int nh = ng + jj * 16 + fk * 4;
-        const uint2 vh = *reinterpret_cast<const uint2*>(g.bias + nh);
-        const uint2 vg = *reinterpret_cast<const uint2*>(g.bias + nh + 32);
-        bh[jj][0] = bf2f(vh.x & 0xffff); bh[jj][1] = bf2f(vh.x >> 16);
-        bh[jj][2] = bf2f(vh.y & 0xffff); bh[jj][3] = bf2f(vh.y >> 16);
-        bg[jj][0] = bf2f(vg.x & 0xffff); bg[jj][1] = bf2f(vg.x >> 16);
-        bg[jj][2] = bf2f(vg.y & 0xffff); bg[jj][3] = bf2f(vg.y >> 16);
-      }
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int ha = 0; ha < 2; ++ha)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int m = m0 + ha * 128 + wr * 32 + i * 16 + fr;
-          if (m >= g.M) continue;
+          for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+    return;
+  }
+  // Epilogue through LDS: the operand ring (128 KB, free once the last phase's barrier has passed and no staging is
+  // in flight) holds the whole 256 x 256 tile as bf16 (acc + bias, rounded once -- the unfused Linear's output),
+  // then every wave stores whole 512-B rows in 16-B chunks (full 128-B lines per instruction) instead of the MFMA
+  // layout's 16 rows x 32 B per store instruction.  Chunk c of row R sits at chunk c ^ (R & 31): the ds_write_b64 of
+  // a 16-row fragment column is 2-way banked, the 16-lane ds_read_b128 of one row is conflict-free.
+  __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
+  bf16_t* tl = l8;
+  auto tix = [](int R, int c) { return R * 256 + ((c ^ (R & 31)) << 3); };  // element index of chunk c of row R
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const int nh = ng + jj * 16 + fk * 4;
-            float vh[4], vg[4], o[4];
+  for (int hb = 0; hb < 2; ++hb) {
+    float bv[4][4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              // h and gate rounded to bf16 first (the unfused path stores them in bf16 before the GEGLU)
-              vh[r] = bf_round(acc[ha][hb][i][jj][r] + bh[jj][r]);
-              vg[r] = bf_round(acc[ha][hb][i][jj + 2][r] + bg[jj][r]);
-              o[r] = vh[r] * gelu_erf(vg[r]);
-            }
-            if (g.out2 && m < g.pre_rows) {
-              bf16_t* p = reinterpret_cast<bf16_t*>(g.out2) + (long)m * g.ldo2 + nh;
-              *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(vh[0], vh[1]), pack2bf(vh[2], vh[3]));
-              *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(vg[0], vg[1]), pack2bf(vg[2], vg[3]));
-            }
-            *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ng / 2 + jj * 16 + fk * 4) =
-                make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
-          }
+    for (int jt = 0; jt < 4; ++jt) {
+      const int n = n0 + hb * 128 + wc * 64 + jt * 16 + fk * 4;
+      const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
+      bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
+      bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
+    }
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int R = ha * 128 + wr * 32 + i * 16 + fr;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+          const int col = hb * 128 + wc * 64 + jt * 16 + fk * 4;
+          const f32x4 a = acc[ha][hb][i][jt];
+          const float al = g.alpha;
+          *reinterpret_cast<uint2*>(tl + tix(R, col >> 3) + (col & 7)) =
+              make_uint2(pack2bf(a[0] * al + bv[jt][0], a[1] * al + bv[jt][1]),
+                         pack2bf(a[2] * al + bv[jt][2], a[3] * al + bv[jt][3]));
         }
+      }
+  }
+  __syncthreads();
+  // 512 threads = 16 rows x 32 chunks per pass, 16 passes
+  const int cq = tid & 31, rq = tid >> 5;
+  if constexpr (EPI == EPI8_GEGLU) {
+    // the staged tile IS the interleaved pre-activation ([h 32 | gate 32] per 64 columns): store its policy rows,
+    // then form out = h * gelu(gate) from it (columns c and c + 32 of each 64-group -> 8 output columns per thread)
+    if (g.out2) {
+#pragma unroll 4
+      for (int p = 0; p < 16; ++p) {
+        const int R = p * 16 + rq, m = m0 + R;
+        if (m < g.pre_rows && m < g.M)
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out2) + (long)m * g.ldo2 + n0 + cq * 8) =
+              *reinterpret_cast<const uint4*>(tl + tix(R, cq));
+      }
+    }
+    // output chunk q (16 per row: 128 output columns) = h chunk (q / 4) * 8 + (q % 4), gate chunk + 4
+    const int q = tid & 15, rr = tid >> 4;  // 32 rows per pass, 8 passes
+    const int ch = (q >> 2) * 8 + (q & 3);
+#pragma unroll 2
+    for (int p = 0; p < 8; ++p) {
+      const int R = p * 32 + rr, m = m0 + R;
+      if (m >= g.M) continue;
+      const uint4 hv = *reinterpret_cast<const uint4*>(tl + tix(R, ch));
+      const uint4 gv = *reinterpret_cast<const uint4*>(tl + tix(R, ch + 4));
+      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = pack2bf(bf2f(hw[e] & 0xffff) * gelu_erf(bf2f(gw[e] & 0xffff)),
+                       bf2f(hw[e] >> 16) * gelu_erf(bf2f(gw[e] >> 16)));
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 / 2 + q * 8) =
+          make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  } else if constexpr (EPI == EPI8_GEGLU_BWD) {
+    // staged tile = dout (bf16, as the unfused path stores it); chunk cq of row R = dout columns n .. n+7 ->
+    // interleaved input-gradient positions ph .. ph+7 (h) and ph+32 .. (gate), ph = (n / 32) * 64 + n % 32
+    const int n = n0 + cq * 8;
+    const int ph = (n >> 5) * 64 + (n & 31);
+#pragma unroll 2
+    for (int p = 0; p < 16; ++p) {
+      const int R = p * 16 + rq, m = m0 + R;
+      if (m >= g.M) continue;
+      const uint4 dv = *reinterpret_cast<const uint4*>(tl + tix(R, cq));
+      const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph);
+      const uint4 gv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph + 32);
+      const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
+      uint32_t oh[4], og[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d0 = bf2f(dw[e] & 0xffff), d1 = bf2f(dw[e] >> 16);
+        const float h0 = bf2f(hw[e] & 0xffff), h1 = bf2f(hw[e] >> 16);
+        const float q0 = bf2f(gw[e] & 0xffff), q1 = bf2f(gw[e] >> 16);
+        float c0, e0, c1, e1;
+        gelu_erf_parts(q0, c0, e0);
+        gelu_erf_parts(q1, c1, e1);
+        oh[e] = pack2bf(d0 * q0 * c0, d1 * q1 * c1);
+        og[e] = pack2bf(d0 * h0 * (c0 + 0.39894228040143268f * q0 * e0), d1 * h1 * (c1 + 0.39894228040143268f * q1 * e1));
+      }
+      bf16_t* o = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
+      *reinterpret_cast<uint4*>(o) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
+      *reinterpret_cast<uint4*>(o + 32) = make_uint4(og[0], og[1], og[2], og[3]);
     }
   } else {
+    const bool has_r = g.resid != nullptr;
+#pragma unroll 4
+    for (int p = 0; p < 16; ++p) {
+      const int R = p * 16 + rq, m = m0 + R;
+      if (m >= g.M) continue;
+      uint4 y = *reinterpret_cast<const uint4*>(tl + tix(R, cq));
+      if (has_r) {  // residual added to the bf16-rounded projection (the unfused Linear + add)
+        const uint4 rv = *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + cq * 8);
+        const uint32_t yw[4] = {y.x, y.y, y.z, y.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+        uint32_t o[4];
 #pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-      float bv[4][4];
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
-        const int n = n0 + hb * 128 + wc * 64 + jt * 16 + fk * 4;
-        const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
-        bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
-        bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
+        for (int e = 0; e < 4; ++e)
+          o[e] = pack2bf(bf2f(yw[e] & 0xffff) + bf2f(rw[e] & 0xffff), bf2f(yw[e] >> 16) + bf2f(rw[e] >> 16));
+        y = make_uint4(o[0], o[1], o[2], o[3]);
       }
-#pragma unroll
-      for (int ha = 0; ha < 2; ++ha)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int m = m0 + ha * 128 + wr * 32 + i * 16 + fr;
-          if (m >= g.M) continue;
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt) {
-            const int n = n0 + hb * 128 + wc * 64 + jt * 16 + fk * 4;
-            const f32x4 a = acc[ha][hb][i][jt];
-            *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n) =
-                make_uint2(pack2bf(a[0] + bv[jt][0], a[1] + bv[jt][1]), pack2bf(a[2] + bv[jt][2], a[3] + bv[jt][3]));
-          }
-        }
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + cq * 8) = y;
     }
   }
 }
@@ -287,21 +382,25 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
 
 }  // namespace
 
-// Host entries used by gemm.hip (preconditions checked there): N % 256 == 0, K % 128 == 0, 16-B aligned rows,
-// M * lda and N * ldw below 2^30 (byte offsets of the buffer loads).
-int pso_gemm8p(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias, void* out,
-               long ldo, int group_m, hipStream_t st) {
-  Gemm8Args g{};
-  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
-  g.M = M; g.N = N; g.K = K; g.bias = (const bf16_t*)bias; g.out = out; g.ldo = ldo; g.group_m = group_m;
-  return launch8<EPI8_NONE>(g, st);
-}
+// Host entries used by gemm.hip (preconditions checked there): N % 256 == 0, K % 64 == 0, 16-B aligned rows, every
+// operand's M * ld (or N * ld) below 2^30 elements (byte offsets of the buffer loads are 32-bit).
+static int g_skip_epi8 = 0;
+extern "C" void pso_gemm8p_skip_epilogue(int on) { g_skip_epi8 = on; }
 
-int pso_gemm8p_geglu(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
-                     void* out, long ldo, void* out_pre, long ld_pre, int pre_rows, int group_m, hipStream_t st) {
+int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2,
+                   long lda2, int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha,
+                   const void* bias, const void* resid, long ldr, void* out, long ldo, void* out2, long ldo2,
+                   int pre_rows, const void* aux, long ldaux, int group_m, hipStream_t st) {
   Gemm8Args g{};
   g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
-  g.M = M; g.N = N; g.K = K; g.bias = (const bf16_t*)bias; g.out = out; g.ldo = ldo;
-  g.out2 = out_pre; g.ldo2 = ld_pre; g.pre_rows = pre_rows; g.group_m = group_m;
-  return launch8<EPI8_GEGLU>(g, st);
+  g.M = M; g.N = N; g.K = K;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0; g.w2 = (const bf16_t*)w2; g.ldw2 = ldw2;
+  g.tail_m = tail_m; g.tail_group_n = a2 ? tail_group_n : 0;
+  g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out2 = out2; g.ldo2 = ldo2; g.pre_rows = pre_rows;
+  g.aux = (const bf16_t*)aux; g.ldaux = ldaux;
+  g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  if (epi == EPI8_GEGLU) return launch8<EPI8_GEGLU>(g, st);
+  if (epi == EPI8_GEGLU_BWD) return launch8<EPI8_GEGLU_BWD>(g, st);
+  return launch8<EPI8_NONE>(g, st);
 }

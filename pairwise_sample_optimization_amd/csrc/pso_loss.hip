@@ -22,6 +22,14 @@ __device__ __forceinline__ float rl(float x) {
   else if constexpr (MODE == PSO_MODE_DMD_BF16) return bf_round(x);
   else return x;
 }
+// An opaque copy: the compiler cannot fuse an operation across it.  Every product / quotient of the step arithmetic
+// goes through one, so the expressions are evaluated exactly as the reference's separate torch element-wise ops (each
+// IEEE-rounded) no matter which contraction mode a translation unit is built with (an FMA of `x - c*e` once flipped a
+// bf16 rounding tie of the DMD2 replay x0 against DP/distilled_inference_with_logprob.py).
+__device__ __forceinline__ float rnd(float x) {
+  asm("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ float rl_rt(int mode, float x) {
   return mode == PSO_MODE_DMD_F16 ? rl<PSO_MODE_DMD_F16>(x) : mode == PSO_MODE_DMD_BF16 ? rl<PSO_MODE_DMD_BF16>(x) : x;
 }
@@ -44,19 +52,19 @@ template <int MODE>
 __device__ __forceinline__ float step_mean(float x, float e, const Coef& k) {
   if (MODE == PSO_MODE_TURBO) {
     const float s = k.c[0];
-    const float pred = x - s * e;
-    const float deriv = (x - pred) / s;
-    return x + deriv * k.c[2];
+    const float pred = x - rnd(s * e);
+    const float deriv = rnd((x - pred) / s);
+    return x + rnd(deriv * k.c[2]);
   } else {  // DP/distilled_inference_with_logprob.py:84-86 (x0 cast to the latent dtype), :112
-    const float x0 = rl<MODE>((x - k.c[1] * e) / k.c[0]);
-    return rl<MODE>(k.c[2] * x0);
+    const float x0 = rl<MODE>(rnd(x - rnd(k.c[1] * e)) / k.c[0]);
+    return rl<MODE>(rnd(k.c[2] * x0));
   }
 }
 // one element of the Gaussian log-density, DP/turbo_inference_with_logprob.py:108-112 / DP/distilled_...:129-133
 template <int MODE>
 __device__ __forceinline__ float lp_term(float pv, float mu, float denom, float lstd, float lc) {
   const float d = rl<MODE>(pv - mu);
-  const float q = rl<MODE>(-rl<MODE>(d * d) / denom);
+  const float q = rl<MODE>(rnd(-rl<MODE>(rnd(d * d)) / denom));
   return rl<MODE>(rl<MODE>(q - lstd) - lc);
 }
 template <int MODE>
@@ -128,7 +136,8 @@ __global__ __launch_bounds__(LP_THREADS) void lp_partial_kernel(
       const float4 z = *reinterpret_cast<const float4*>(noise + nb);
       const float zs[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pv[j] = MODE == PSO_MODE_TURBO ? mu[j] + zs[j] * std : rl<MODE>(mu[j] + rl<MODE>(std * zs[j]));
+      for (int j = 0; j < 4; ++j)
+        pv[j] = MODE == PSO_MODE_TURBO ? mu[j] + rnd(zs[j] * std) : rl<MODE>(mu[j] + rl<MODE>(rnd(std * zs[j])));
       *reinterpret_cast<float4*>(prev_out + base + i) = make_float4(pv[0], pv[1], pv[2], pv[3]);
     }
 #pragma unroll

@@ -30,13 +30,16 @@ def turbo_coef(sigmas, timesteps, t):
     nxt = [i + 1 for i in idx]
     s_from = sigmas[idx]
     s_to = sigmas[nxt]
-    s_up = (s_to ** 2 * (s_from ** 2 - s_to ** 2) / s_from ** 2) ** 0.5
-    s_down = (s_to ** 2 - s_up ** 2) ** 0.5
+    # `** 2` / `** 0.5` of the reference as explicit x*x and IEEE sqrt: torch's CPU pow kernels differ by an ulp
+    # between host CPUs (vectorised pow vs sqrt), sqrt is correctly rounded everywhere
+    sq = lambda v: v * v
+    s_up = torch.sqrt(sq(s_to) * (sq(s_from) - sq(s_to)) / sq(s_from))
+    s_down = torch.sqrt(sq(s_to) - sq(s_up))
     c = torch.zeros(len(idx), COEF_STRIDE, dtype=torch.float32)
     c[:, 0] = s_from
     c[:, 1] = s_up
     c[:, 2] = s_down - s_from
-    c[:, 3] = 2 * (s_up ** 2)
+    c[:, 3] = 2 * sq(s_up)
     c[:, 4] = torch.log(s_up)
     c[:, 5] = LOG_SQRT_2PI
     return c
@@ -59,28 +62,31 @@ def dmd_coef(alphas_cumprod, t, t_prev, latent_dtype=torch.float32):
     a_t = ac[torch.as_tensor(t).reshape(-1).long().cpu()]
     tp = torch.as_tensor(t_prev).reshape(-1).long().cpu()
     a_p = ac[tp]
+    # `** 0.5` as IEEE sqrt (correctly rounded on every host; torch's CPU pow may not be), and in the latent dtype
+    # as the fp32 sqrt rounded once to it (what torch's reduced-precision pow computes)
+    rsqrt = lambda v: torch.sqrt(v.float()).to(v.dtype)
     if latent_dtype in DMD_REPLAY_MODES:
         acl = ac.to(latent_dtype)
-        sa_l = acl[tp] ** 0.5
-        sb_l = (1 - acl[tp]) ** 0.5
+        sa_l = rsqrt(acl[tp])
+        sb_l = rsqrt(1 - acl[tp])
         c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
-        c[:, 0] = a_t ** 0.5
-        c[:, 1] = (1 - a_t) ** 0.5
+        c[:, 0] = torch.sqrt(a_t)
+        c[:, 1] = torch.sqrt(1 - a_t)
         c[:, 2] = sa_l.float()
         c[:, 3] = sb_l.float()
-        c[:, 4] = (2 * (sb_l ** 2)).float()
+        c[:, 4] = (2 * (sb_l * sb_l)).float()
         c[:, 5] = torch.log(sb_l).float()
         # `- torch.log(torch.sqrt(2 * torch.as_tensor(math.pi)))` (:132): the fp32 0-dim tensor meets a latent-dtype
         # tensor and is cast to that dtype first
         c[:, 6] = torch.tensor(LOG_SQRT_2PI).to(latent_dtype).float()
         return c
-    sbp = (1 - a_p) ** 0.5
+    sbp = torch.sqrt(1 - a_p)
     c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
-    c[:, 0] = a_t ** 0.5
-    c[:, 1] = (1 - a_t) ** 0.5
-    c[:, 2] = a_p ** 0.5
+    c[:, 0] = torch.sqrt(a_t)
+    c[:, 1] = torch.sqrt(1 - a_t)
+    c[:, 2] = torch.sqrt(a_p)
     c[:, 3] = sbp
-    c[:, 4] = 2 * (sbp ** 2)
+    c[:, 4] = 2 * (sbp * sbp)
     c[:, 5] = torch.log(sbp)
     c[:, 6] = LOG_SQRT_2PI
     return c

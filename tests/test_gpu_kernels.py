@@ -160,7 +160,7 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 30, 31, 41])
 @pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
                                         (8192, 640, 320, 0), (1000, 700, 136, 0)])
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
@@ -209,6 +209,75 @@ def test_gemm_8phase(cuda, M, N, K):
         K_.gemm(a, w, bias=b, out=out)
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(4096, 3840, 1280, 32, 1280, 2048), (1000, 768, 640, 32, 256, 0),
+                                                      (4100, 1024, 640, 96, 0, 4100), (520, 512, 192, 32, 512, 300),
+                                                      (16384, 3840, 1280, 32, 1280, 8192)])
+def test_gemm_8phase_lora_tail_paired_resid(cuda, M, N, K, K2, group, tail_rows):
+    """gemm8p with the LoRA K-tail (grouped per output-column block, or plain), restricted to the first tail_rows rows
+    (the policy half of a paired pass), alpha, bias and a residual epilogue; odd / even K-tile counts."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(30)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K + K2)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        b = torch.randn(N, device=cuda, generator=g).bfloat16()
+        r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+        tr = tail_rows or M
+        ng = N // group if group else 1
+        u = torch.randn(tr, K2 * ng, device=cuda, generator=g).bfloat16()
+        w2 = (torch.randn(N, K2, device=cuda, generator=g) / 6).bfloat16()
+        y = a.float() @ w.float().t()
+        for j in range(ng):
+            cs = slice(j * group, (j + 1) * group) if group else slice(0, N)
+            y[:tr, cs] += u[:, K2 * j:K2 * (j + 1)].float() @ w2[cs].float().t()
+        ref = (0.75 * y + b.float()).bfloat16().float() + r.float()
+        sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+        out = sentinel[:M]
+        K_.gemm(a, w, bias=b, resid=r, a2=u, w2=w2, alpha=0.75, tail_group_n=group, tail_rows=tail_rows, out=out)
+        assert _rel(out, ref) < 4e-3
+        assert _rel(out[tr:], ref[tr:]) < 4e-3 if tr < M else True
+        assert (sentinel[M:] == 7.0).all()
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 31])
+@pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100)])
+def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
+    """The GEGLU projection (interleaved [h | gate] weight rows) and its backward through ff.net.2, on the 8-phase
+    path (default) and the 2-phase one (variant 31), against torch fp32 on the same bf16 operands."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(variant)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + Fd)
+        x = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        wp = (torch.randn(2 * Fd, K, device=cuda, generator=g) / K ** 0.5).bfloat16()  # diffusers [h rows; gate rows]
+        bp = torch.randn(2 * Fd, device=cuda, generator=g).bfloat16()
+        idx = K_.geglu_interleave_index(Fd, cuda)
+        pr = pre_rows or M
+        pre = torch.empty(pr, 2 * Fd, device=cuda, dtype=torch.bfloat16)
+        out = K_.gemm_geglu(x, wp[idx].contiguous(), bp[idx].contiguous(), out_pre=pre, pre_rows=pre_rows)
+        hg = (x.float() @ wp.float().t() + bp.float()).bfloat16().float()
+        h, gt = hg[:, :Fd], hg[:, Fd:]
+        assert _rel(out, h * F.gelu(gt)) < 4e-3
+        assert _rel(pre, hg[:pr, idx]) < 4e-3
+        # backward: dout = dy @ W_out^T-form operand [Fd, C] given as w [Fd][C]; din interleaved
+        C = K
+        dy = torch.randn(M, C, device=cuda, generator=g).bfloat16()
+        wo = (torch.randn(Fd, C, device=cuda, generator=g) / C ** 0.5).bfloat16()
+        full_pre = hg[:, idx].bfloat16()
+        din = K_.gemm_geglu_bwd(dy, wo, full_pre)
+        dout = (dy.float() @ wo.float().t()).bfloat16().float()
+        hh, gg = h, gt
+        cdf = 0.5 * (1 + torch.erf(gg / 2 ** 0.5))
+        pdf = torch.exp(-0.5 * gg * gg) / (2 * torch.pi) ** 0.5
+        ref = torch.cat([dout * gg * cdf, dout * hh * (cdf + gg * pdf)], 1)[:, idx]
+        assert _rel(din, ref) < 6e-3
     finally:
         K_.lib().pso_gemm_set_variant(0)
 

@@ -38,3 +38,15 @@ for k in range(2):
         pr = rl(mean + rl(np.float32(sb_p[b]) * np.float32(Z)))
         print(" idx", i, "x", X, "eps", E, "z", Z, "x0f", x0f, "x0", x0, "mean", mean, "oracle prev", pr,
               "ref prev", d[f"prev{k}"][i], "gpu prev", g[i])
+
+# fp32 x0 of the failing element straight from the kernel: DMD mode, c2 = 1, zero noise -> prev = x0 (unrounded)
+c = coef.clone()
+c[:, 2] = 1.0
+for k in range(2):
+    x = torch.from_numpy(d[f"x{k}"]).to(dev)
+    e = torch.from_numpy(d[f"eps_ref{k}"]).to(dev)
+    prev, _ = K.step_logprob(1, x, e, c, noise=torch.zeros_like(x[:1]), noise_shared=True)
+    g = prev.cpu().numpy()
+    x0f = (d[f"x{k}"] - sb.reshape(-1, 1, 1, 1) * d[f"eps_ref{k}"]) / sa.reshape(-1, 1, 1, 1)
+    bad = np.argwhere(g != x0f)
+    print("fp32 x0 mismatches", k, len(bad), [(tuple(i), g[tuple(i)], x0f[tuple(i)]) for i in bad[:4]])

@@ -16,6 +16,8 @@ def main():
     args = bench.parse()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if os.environ.get("PSO_BENCH_GEMM_VARIANT"):
+        K.lib().pso_gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
     unet, tr, buf, g = bench.build(args, dev)
     bench.one_step(tr, buf, g)
     torch.cuda.synchronize()
@@ -32,7 +34,8 @@ def main():
         a[2] += fl
     tot = sum(a[1] for a in agg.values())
     print(f"GEMM family: {len(rec)} launches, {tot:.1f} ms, {sum(a[2] for a in agg.values()) / tot / 1e9:.1f} TF/s")
-    for tag, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60]:
+    top = int(os.environ.get("SHAPE_TOP", "60"))
+    for tag, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         print(f"{ms:8.2f} ms {100 * ms / tot:5.1f}% n={n:4d} {fl / ms / 1e9:7.1f} TF/s  {tag}")
 
 
