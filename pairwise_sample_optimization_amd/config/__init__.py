@@ -45,3 +45,50 @@ def _common():
         "per_prompt_stat_tracking": {"buffer_size": 16, "min_count": 16},
         "kl_ratio": 0.01, "prompt_fn": "simple_animals", "prompt_fn_kwargs": {},
     }
+
+
+def load_config_file(path):
+    """Execute a run config in the reference's own format -- e.g. the reference's
+    `human_preference_tuning/config/config_sdxl_turbo_dpo.py` unchanged (`import ml_collections`,
+    `config = ml_collections.ConfigDict()`, nested `config.sample = ml_collections.ConfigDict()`, `get_config()`) --
+    with this module's ConfigDict standing in for the absent ml_collections package (T:55-56 loads it through absl's
+    config_flags.DEFINE_config_file).  Returns the ConfigDict."""
+    import importlib.util
+    import sys
+    import types
+    stub = types.ModuleType("ml_collections")
+    stub.ConfigDict = ConfigDict
+    saved = sys.modules.get("ml_collections")
+    sys.modules["ml_collections"] = stub
+    try:
+        spec = importlib.util.spec_from_file_location("_pso_run_config", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod.get_config()
+    finally:
+        if saved is None:
+            del sys.modules["ml_collections"]
+        else:
+            sys.modules["ml_collections"] = saved
+
+
+def apply_overrides(cfg, overrides):
+    """absl config_flags overrides as the launch scripts pass them (`--config.train.beta=50`,
+    online_pso_sdxl_turbo.sh:4-15): each item "a.b.c=value" (a leading "--config." is stripped); values are Python
+    literals where they parse as one, else strings."""
+    import ast
+    for item in overrides:
+        key, _, val = item.partition("=")
+        key = key[len("--config."):] if key.startswith("--config.") else key
+        try:
+            v = ast.literal_eval(val)
+        except (ValueError, SyntaxError):
+            v = val
+        node = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            node = getattr(node, p)
+        if parts[-1] not in node:
+            raise KeyError(f"config has no field {key!r}")
+        node[parts[-1]] = v
+    return cfg

@@ -796,8 +796,10 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if (ks < 1) ks = 1;
     return launch<64, 64>(g, st, (int)ks);
   }
-  // 8-phase 256x256 (gemm8p.hip) for every dense bf16 GEMM with N % 256 == 0 and enough tiles to fill the chip:
-  // LDS-staged 16-B epilogue, LoRA K-tail, bias / alpha / residual.  Variant 31 keeps the 2-phase kernels (A/B knob).
+  // 8-phase 256x256 (gemm8p.hip) for dense bf16 GEMMs with N % 256 == 0: LDS-staged 16-B epilogue, LoRA K-tail,
+  // bias / alpha / residual.  Opt-in (variant 30 / 32): inside the C2 step it measured equal to the 2-phase kernels on
+  // the q/k/v projection (983 vs 971 TF/s, 16384 x 3840 x 1280 + tail) while the GEMM that follows it slowed down by
+  // about what it saved (its output's dirty lines are written back during the next kernel), tools/shape_prof.py.
   const bool ok8 = !g.conv.mode && !g.rowbias && g.out_dtype == PSO_BF16 && !g.accumulate && (g.N % 256) == 0 &&
                    (g.K1 % 64) == 0 && al16(g.a1) && al16(g.b1) && (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 &&
                    al16(g.out) && (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
@@ -805,7 +807,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
                    (!g.a2 || ((g.tail_group_n == 0 || (g.tail_group_n % 256) == 0) && fits30(g.tail_m, g.lda2) &&
                               fits30(g.N, g.ldb2)));
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
-  if (ok8 && gv != 31 && (gv == 30 || (gv == 0 && t256 >= 256)))
+  if (ok8 && (gv == 30 || (gv == 32 && t256 >= 256)))
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);
@@ -1048,7 +1050,8 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   // the 8-phase kernel with the LDS-staged epilogue (gemm8p.hip): 16384 x 10240 x 1280 1023 vs 801 TF/s,
-  // 65536 x 5120 x 640 814 vs 640 (tools/gemm_bench.py, one box); variant 31 keeps the 2-phase 256x256 kernel
+  // 65536 x 5120 x 640 814 vs 640 (tools/gemm_bench.py, one box), inside the C2 step 1006 vs 922 / 801 vs 706
+  // (tools/shape_prof.py); variant 31 keeps the 2-phase 256x256 kernel
   if (g_gemm_variant != 31 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw))
     return pso_gemm8p_run(1, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, bias, nullptr, 0, out, ldo,
                           out_pre, ld_pre, g.tail_m, nullptr, 0, g.group_m, (hipStream_t)stream);
@@ -1077,8 +1080,9 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   const hipStream_t st = (hipStream_t)stream;
-  if (g_gemm_variant != 31 && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw) &&
-      (long)((M + 255) / 256) * (N / 256) >= 128)
+  // 8-phase form opt-in (variant 30 / 32): 623 vs 660 TF/s for the 2-phase 128x160 kernel at 8192 x 5120 x 1280
+  if ((g_gemm_variant == 30 || g_gemm_variant == 32) && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) &&
+      fits30(N, ldw) && (long)((M + 255) / 256) * (N / 256) >= 128)
     return pso_gemm8p_run(2, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, nullptr, nullptr, 0, out,
                           ldo, nullptr, 0, 0, pre, ld_pre, g.group_m, st);
   const long t160 = (long)((M + 127) / 128) * ((N + 159) / 160);

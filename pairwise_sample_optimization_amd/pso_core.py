@@ -21,6 +21,13 @@ def _f32(x):
     return torch.as_tensor(x, dtype=torch.float32).cpu()
 
 
+def _sqrt(v):
+    """IEEE-exact float32 sqrt on any host: the float64 sqrt rounded to float32 (exact for sqrt, p64 >= 2 p32 + 2).
+    torch's float32 CPU sqrt is NOT exact on every host CPU (a vectorised path on one GPU box returned 0x3f599312 for
+    sqrt(0.72233057), correct 0x3f599311), which would move the DMD2 replay x0 across a bf16 rounding tie."""
+    return torch.sqrt(v.double()).to(v.dtype)
+
+
 def turbo_coef(sigmas, timesteps, t):
     """Per-sample [sigma, sigma_up, sigma_down - sigma, 2 sigma_up^2, log sigma_up, log sqrt(2 pi), 0, 0] (float32)."""
     sigmas = _f32(sigmas)
@@ -33,8 +40,8 @@ def turbo_coef(sigmas, timesteps, t):
     # `** 2` / `** 0.5` of the reference as explicit x*x and IEEE sqrt: torch's CPU pow kernels differ by an ulp
     # between host CPUs (vectorised pow vs sqrt), sqrt is correctly rounded everywhere
     sq = lambda v: v * v
-    s_up = torch.sqrt(sq(s_to) * (sq(s_from) - sq(s_to)) / sq(s_from))
-    s_down = torch.sqrt(sq(s_to) - sq(s_up))
+    s_up = _sqrt(sq(s_to) * (sq(s_from) - sq(s_to)) / sq(s_from))
+    s_down = _sqrt(sq(s_to) - sq(s_up))
     c = torch.zeros(len(idx), COEF_STRIDE, dtype=torch.float32)
     c[:, 0] = s_from
     c[:, 1] = s_up
@@ -62,16 +69,16 @@ def dmd_coef(alphas_cumprod, t, t_prev, latent_dtype=torch.float32):
     a_t = ac[torch.as_tensor(t).reshape(-1).long().cpu()]
     tp = torch.as_tensor(t_prev).reshape(-1).long().cpu()
     a_p = ac[tp]
-    # `** 0.5` as IEEE sqrt (correctly rounded on every host; torch's CPU pow may not be), and in the latent dtype
+    # `** 0.5` as IEEE sqrt (correctly rounded on every host; torch's CPU pow / sqrt may not be), and in the latent dtype
     # as the fp32 sqrt rounded once to it (what torch's reduced-precision pow computes)
-    rsqrt = lambda v: torch.sqrt(v.float()).to(v.dtype)
+    rsqrt = lambda v: _sqrt(v.float()).to(v.dtype)
     if latent_dtype in DMD_REPLAY_MODES:
         acl = ac.to(latent_dtype)
         sa_l = rsqrt(acl[tp])
         sb_l = rsqrt(1 - acl[tp])
         c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
-        c[:, 0] = torch.sqrt(a_t)
-        c[:, 1] = torch.sqrt(1 - a_t)
+        c[:, 0] = _sqrt(a_t)
+        c[:, 1] = _sqrt(1 - a_t)
         c[:, 2] = sa_l.float()
         c[:, 3] = sb_l.float()
         c[:, 4] = (2 * (sb_l * sb_l)).float()
@@ -80,11 +87,11 @@ def dmd_coef(alphas_cumprod, t, t_prev, latent_dtype=torch.float32):
         # tensor and is cast to that dtype first
         c[:, 6] = torch.tensor(LOG_SQRT_2PI).to(latent_dtype).float()
         return c
-    sbp = torch.sqrt(1 - a_p)
+    sbp = _sqrt(1 - a_p)
     c = torch.zeros(a_t.shape[0], COEF_STRIDE, dtype=torch.float32)
-    c[:, 0] = torch.sqrt(a_t)
-    c[:, 1] = torch.sqrt(1 - a_t)
-    c[:, 2] = torch.sqrt(a_p)
+    c[:, 0] = _sqrt(a_t)
+    c[:, 1] = _sqrt(1 - a_t)
+    c[:, 2] = _sqrt(a_p)
     c[:, 3] = sbp
     c[:, 4] = 2 * (sbp * sbp)
     c[:, 5] = torch.log(sbp)

@@ -800,7 +800,9 @@ class UNet2DConditionModel(nn.Module):
         self.cfg = cfg
         self.config = SimpleNamespace(in_channels=cfg.in_channels, out_channels=cfg.out_channels,
                                       sample_size=cfg.sample_size, block_out_channels=cfg.block_out_channels,
-                                      cross_attention_dim=cfg.cross_attention_dim)
+                                      cross_attention_dim=cfg.cross_attention_dim,
+                                      addition_time_embed_dim=cfg.addition_time_embed_dim,
+                                      projection_class_embeddings_input_dim=cfg.projection_class_embeddings_input_dim)
         ch = cfg.block_out_channels
         G, eps, tdim = cfg.norm_num_groups, cfg.norm_eps, cfg.time_embed_dim
         self.conv_in = Conv2d(cfg.in_channels, ch[0], 3)
@@ -879,7 +881,36 @@ class UNet2DConditionModel(nn.Module):
 
     @classmethod
     def from_config(cls, config=None, **kw):
-        return cls(config if isinstance(config, UNetConfig) else UNetConfig.sdxl())
+        """`UNet2DConditionModel.from_config(cfg)` (D:313-318): a UNetConfig, or a diffusers config dict (the keys of
+        `unet/config.json`, validated against what the kernels implement: diffusers_io.unet_config_from_diffusers);
+        None -> SDXL.  Weights are left uninitialised, as diffusers leaves them before load_state_dict."""
+        from . import diffusers_io
+        if config is None:
+            config = UNetConfig.sdxl()
+        elif isinstance(config, dict):
+            config = diffusers_io.unet_config_from_diffusers(dict(config, **kw))
+        elif not isinstance(config, UNetConfig):
+            raise TypeError(f"from_config takes a UNetConfig or a diffusers config dict, not {type(config).__name__}")
+        return cls(config)
+
+    @classmethod
+    def load_config(cls, path, subfolder=None, **kw):
+        from . import diffusers_io
+        return diffusers_io.load_config(path, subfolder)
+
+    @classmethod
+    def from_pretrained(cls, path, subfolder=None, torch_dtype=None, variant=None, revision=None, **kw):
+        """`UNet2DConditionModel.from_pretrained(path, subfolder="unet")` (T:290) from a local diffusers directory:
+        config.json + diffusion_pytorch_model[.variant].safetensors (bf16 weights; torch_dtype / revision are
+        accepted for API parity -- the kernels compute in bf16)."""
+        from . import diffusers_io
+        model = cls.from_config(diffusers_io.load_config(path, subfolder))
+        model.load_state_dict(diffusers_io.load_weights(path, subfolder, variant))
+        return model
+
+    def save_pretrained(self, path):
+        from . import diffusers_io
+        diffusers_io.save_pretrained(self, path, diffusers_io.unet_config_to_diffusers(self.cfg))
 
     def init_weights(self, seed=0):
         """PyTorch-default-style seeded init (the BASELINE synthetic-weights recipe); norms at identity."""

@@ -170,6 +170,26 @@ class AutoencoderKL(nn.Module):
         self.decoder = Decoder(self.cfg)
         self._prepared = False
 
+    @classmethod
+    def from_config(cls, config=None, **kw):
+        """A VAEConfig or a diffusers AutoencoderKL config dict (validated: diffusers_io.vae_config_from_diffusers)."""
+        from . import diffusers_io
+        if isinstance(config, dict):
+            config = diffusers_io.vae_config_from_diffusers(dict(config, **kw))
+        return cls(config)
+
+    @classmethod
+    def from_pretrained(cls, path, subfolder=None, torch_dtype=None, variant=None, revision=None, **kw):
+        """`AutoencoderKL.from_pretrained(vae_path, subfolder=...)` (T:273-284) from a local diffusers directory."""
+        from . import diffusers_io
+        model = cls.from_config(diffusers_io.load_config(path, subfolder))
+        model.load_state_dict(diffusers_io.load_weights(path, subfolder, variant))
+        return model
+
+    def save_pretrained(self, path):
+        from . import diffusers_io
+        diffusers_io.save_pretrained(self, path, diffusers_io.vae_config_to_diffusers(self.cfg))
+
     def init_weights(self, seed=0):
         g = torch.Generator(device=self.post_quant_conv.weight.device).manual_seed(seed)
         for m in self.modules():

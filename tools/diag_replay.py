@@ -15,7 +15,12 @@ lat = torch.bfloat16
 dev = torch.device("cuda")
 coef = pso_core.dmd_coef(torch.from_numpy(d["alphas_cumprod"]), torch.from_numpy(d["t"]), torch.from_numpy(d["t_prev"]),
                          latent_dtype=lat).to(dev)
-print("coef", coef.cpu().numpy())
+print("coef", coef.cpu().numpy(), [hex(v) for v in coef.cpu().numpy().view(np.uint32)[0, :4]])
+print("np  ", [hex(v) for v in np.array([np.sqrt(np.float32(d["alphas_cumprod"][499])),
+                                          np.sqrt(np.float32(1) - np.float32(d["alphas_cumprod"][499]))],
+                                         np.float32).view(np.uint32)])
+print("torch", torch.__version__, [hex(v) for v in torch.sqrt(1 - torch.tensor([d["alphas_cumprod"][499]])).numpy().view(np.uint32)],
+      [hex(v) for v in ((1 - torch.tensor([d["alphas_cumprod"][499]])) ** 0.5).numpy().view(np.uint32)])
 sa, sb, _, _ = pm.dmd_coefs(d["alphas_cumprod"], d["t"], d["t_prev"])
 sa_p, sb_p, den, lstd = pm.dmd_coefs_latent(d["alphas_cumprod"], d["t_prev"], "bf16")
 print("oracle", sa, sb, sa_p, sb_p, den, lstd)
