@@ -50,7 +50,10 @@ def test_step_and_pair_loss_vs_golden(cuda, path):
     g = K_.pair_loss_bwd(mode, x, xp, ep, coef2, pref, float(d["beta"]), float(d["clip_eps"]), ws, grad_out=go,
                          grad_scale=0.5, out_dtype=torch.float32)
     g = g.reshape((P, 2) + d["x0"].shape[1:]).cpu().numpy()
+    # fp32 kernel vs torch autograd through the reference step: agree to a few 1e-6 of the largest entry; the DMD2
+    # t = 999 case multiplies the mean's rounding by sqrt(abar_prev) sqrt(1-abar_t) / sqrt(abar_t) = 3.4 (measured
+    # 1.01e-5 of max once the step's products were made contraction-free), hence 2e-5
     for k in range(2):
         ref = d[f"grad_eps_pol{k}"]
         scale = max(np.abs(ref).max(), 1e-30)
-        assert np.abs(g[:, k] - ref).max() <= 1e-5 * scale + 1e-12
+        assert np.abs(g[:, k] - ref).max() <= 2e-5 * scale + 1e-12
