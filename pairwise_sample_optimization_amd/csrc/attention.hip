@@ -294,6 +294,260 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd_kernel(AttnArgs a, in
 }
 
 // ================================================================================================================
+// forward v2: the same tiling with the per-tile vector work cut to what the math needs (the loop above issues ~390
+// non-MFMA vector instructions per wave and tile, measured SQ_INSTS_VALU; the vector issue, not the matrix pipe, bounds
+// it at two waves per SIMD):
+//  * the tile loop is unrolled by the ring depth, so every LDS address is a lane base + an immediate (no per-tile
+//    ring-slot arithmetic);
+//  * row maxima by v_max3_f32 in inline asm (fmaxf on MFMA results makes hipcc canonicalise each operand first:
+//    3 instructions per 2 scores instead of 1);
+//  * deferred rescale: the running max moves only when some row of the wave grew by more than RESCALE_LOG2 (in
+//    log2 units), so P <= 2^RESCALE_LOG2 (exact in fp32, rounded to bf16 like every P) and the O / l rescale (and its
+//    branch) is skipped on almost every tile after the first few; one wave-uniform decision covers all QI row groups.
+// Output and LSE are the same function of the inputs: l and O carry the same scale, and LSE = m*c + log2(l).
+// ================================================================================================================
+#define ATT_RESCALE_LOG2 8.0f
+
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float rowmax4_asm(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+template <int V> struct ic { static constexpr int value = V; };
+
+// 8 transposed V reads (inline asm, see tr_read_asm) and the wait that makes their registers available: the wait takes
+// the fragments as in/out operands, so no consumer can be scheduled above it
+__device__ __forceinline__ void lds_wait8(s16x4 (&v)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+}
+
+// transposed read at a lane base + a compile-time byte offset (ring slot and row block fold into the immediate, so a
+// handful of base registers serve every read of the loop)
+template <int OFF>
+__device__ __forceinline__ s16x4 tr_read_imm(unsigned base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
+  return v;
+}
+
+template <int QI>
+__global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, int nqb) {
+  constexpr int STG = 3;
+  constexpr int PIECES = 4;
+  __shared__ __attribute__((aligned(16))) bf16_t sKV[STG][2][ATT_KT * ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qb = bid % nqb, bh = bid / nqb;
+  const int h = bh % a.H, b = bh / a.H;
+  const int q0 = qb * (64 * QI) + wave * (16 * QI);
+
+  const bf16_t* Q = a.q + b * a.sq_b + h * ATT_D;
+  const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
+  const bf16_t* V = a.v + b * a.sv_b + h * ATT_D;
+  const float c2 = a.scale_log2;
+  const float thr = ATT_RESCALE_LOG2 / c2;  // raw-score growth that triggers a rescale
+
+  // K/V staging by buffer_load ... lds against per-(batch, head) SGPR resources whose range ends at key row Sk - 1:
+  // rows past the end read as zeros (masked on the last tile), so the per-lane part of every staging address is one
+  // loop-invariant 32-bit offset and the tile advance is the scalar soffset
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcK = pch ^ prow;
+  const int lcV = pch ^ (2 * ((prow >> 1) & 3));
+  const int nkt = (a.Sk + ATT_KT - 1) / ATT_KT;
+  const __amdgpu_buffer_rsrc_t rK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, (int)(((long)(a.Sk - 1) * a.ldk + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV =
+      __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, (int)(((long)(a.Sk - 1) * a.ldv + ATT_D) * 2), 0x00020000);
+  unsigned kvo[2], vvo[2];
+#pragma unroll
+  for (int pw = 0; pw < 2; ++pw) {
+    const int row = (wave * 2 + pw) * 8 + prow;
+    kvo[pw] = (unsigned)(row * (int)a.ldk + lcK * 8) * 2u;
+    vvo[pw] = (unsigned)(row * (int)a.ldv + lcV * 8) * 2u;
+  }
+  const int kstep = ATT_KT * (int)a.ldk * 2, vstep = ATT_KT * (int)a.ldv * 2;  // bytes per key tile
+  // lane bases of the transposed V reads, one per 16-column block dt (rows 4g.. of slot 0's V image; the ring slot and
+  // the 16-row block are immediates)
+  unsigned vbase[4];
+  {
+    const unsigned lds0 = (unsigned)(uintptr_t)(const att_lds_void*)&sKV[0][0][0];
+    const int li = lane & 15, q = li >> 2, p = li & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int col = dt * 16 + 4 * p;
+      vbase[dt] = lds0 + 2u * (unsigned)(swz_tr(4 * g + q, col >> 3) + (col & 7));
+    }
+  }
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int pw = 0; pw < 2; ++pw) {
+      const int piece = wave * 2 + pw;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sKV[buf][0] + piece * 8 * ATT_D), 16, kvo[pw],
+                                               kt * kstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (att_lds_void*)(sKV[buf][1] + piece * 8 * ATT_D), 16, vvo[pw],
+                                               kt * vstep, 0, 0);
+    }
+  };
+
+  bf16x8 qf[QI][2];
+#pragma unroll
+  for (int qi = 0; qi < QI; ++qi) {
+    const int qr = min(q0 + qi * 16 + c, a.Sq - 1);
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds)
+      qf[qi][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Q + (long)qr * a.ldq + ds * 32 + 8 * g));
+  }
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+
+  f32x4 o[QI][4];
+  f32x4 lsum[QI];
+  float m_run[QI];
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+#pragma unroll
+  for (int qi = 0; qi < QI; ++qi) {
+    m_run[qi] = -INFINITY;
+    lsum[qi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[qi][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  auto tile = [&](auto bufc, int kt) {
+    constexpr int buf = decltype(bufc)::value;
+    if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < nkt) issue(kt + 2, (buf + 2) % STG);
+    const bf16_t* k_img = sKV[buf][0];
+    f32x4 s[QI][4];
+#pragma unroll
+    for (int kj = 0; kj < 4; ++kj) {
+      bf16x8 kf[2];
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+        kf[ds] = *reinterpret_cast<const bf16x8*>(k_img + swz_row(kj * 16 + c, ds * 4 + g));
+#pragma unroll
+      for (int qi = 0; qi < QI; ++qi) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qi][0], acc, 0, 0, 0);
+        s[qi][kj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qi][1], acc, 0, 0, 0);
+      }
+    }
+    // V fragments of the first 32 keys: in flight during the softmax
+    constexpr int VOFF = (buf * 2 + 1) * ATT_KT * ATT_D * 2;  // byte offset of this slot's V image
+    s16x4 vr0[8];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      vr0[2 * dt] = tr_read_imm<VOFF + 0 * 2048>(vbase[dt]);
+      vr0[2 * dt + 1] = tr_read_imm<VOFF + 1 * 2048>(vbase[dt]);
+    }
+    const int kbase = kt * ATT_KT;
+    if (kbase + ATT_KT > a.Sk) {
+#pragma unroll
+      for (int qi = 0; qi < QI; ++qi)
+#pragma unroll
+        for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kbase + kj * 16 + 4 * g + r >= a.Sk) s[qi][kj][r] = -INFINITY;
+    }
+    float mx[QI];
+    bool grow = false;
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) {
+      float m = vmax3(s[qi][0][0], s[qi][0][1], s[qi][0][2]);
+      m = vmax3(m, s[qi][0][3], s[qi][1][0]);
+      m = vmax3(m, s[qi][1][1], s[qi][1][2]);
+      m = vmax3(m, s[qi][1][3], s[qi][2][0]);
+      m = vmax3(m, s[qi][2][1], s[qi][2][2]);
+      m = vmax3(m, s[qi][2][3], s[qi][3][0]);
+      m = vmax3(m, s[qi][3][1], s[qi][3][2]);
+      m = vmax2(m, s[qi][3][3]);
+      mx[qi] = rowmax4_asm(m);
+      grow |= mx[qi] > m_run[qi] + thr;
+    }
+    if (__any(grow)) {  // wave-uniform; every tile while m_run = -inf, rarely afterwards
+#pragma unroll
+      for (int qi = 0; qi < QI; ++qi) {
+        const float m_new = fmaxf(m_run[qi], mx[qi]);
+        const float alpha = fast_exp2((m_run[qi] - m_new) * c2);  // first tile: exp2(-inf) = 0
+        lsum[qi] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qi][dt] *= alpha;
+        m_run[qi] = m_new;
+      }
+    }
+#pragma unroll
+    for (int qi = 0; qi < QI; ++qi) {
+      const float mc = m_run[qi] * c2;
+#pragma unroll
+      for (int kj = 0; kj < 4; ++kj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[qi][kj][r] = fast_exp2(fmaf(s[qi][kj][r], c2, -mc));
+    }
+    lds_wait8(vr0);
+    s16x4 vr1[8];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      vr1[2 * dt] = tr_read_imm<VOFF + 2 * 2048>(vbase[dt]);
+      vr1[2 * dt + 1] = tr_read_imm<VOFF + 3 * 2048>(vbase[dt]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 1) lds_wait8(vr1);
+      bf16x8 pf[QI];
+#pragma unroll
+      for (int qi = 0; qi < QI; ++qi) {
+        pf[qi] = pack_p(s[qi][2 * ks], s[qi][2 * ks + 1]);
+        lsum[qi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qi], lsum[qi], 0, 0, 0);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vf = ks == 0 ? cat_frag(vr0[2 * dt], vr0[2 * dt + 1]) : cat_frag(vr1[2 * dt], vr1[2 * dt + 1]);
+#pragma unroll
+        for (int qi = 0; qi < QI; ++qi) o[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qi], o[qi][dt], 0, 0, 0);
+      }
+    }
+  };
+  for (int kt = 0; kt < nkt; kt += STG) {
+    tile(ic<0>{}, kt);
+    if (kt + 1 < nkt) tile(ic<1>{}, kt + 1);
+    if (kt + 2 < nkt) tile(ic<2>{}, kt + 2);
+  }
+
+  bf16_t* O = a.o + b * a.so_b + h * ATT_D;
+#pragma unroll
+  for (int qi = 0; qi < QI; ++qi) {
+    const float l = lsum[qi][0];
+    const int qr = q0 + qi * 16 + c;
+    if (qr >= a.Sq) continue;
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f32x4 v = o[qi][dt];
+      *reinterpret_cast<uint2*>(O + (long)qr * a.ldo + dt * 16 + 4 * g) =
+          make_uint2(pack2bf(v[0] * inv, v[1] * inv), pack2bf(v[2] * inv, v[3] * inv));
+    }
+    if (a.lse && g == 0)
+      a.lse[((long)b * a.H + h) * a.Sq + qr] = (m_run[qi] * c2 + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
+// ================================================================================================================
 // backward dK/dV: one workgroup = 4 waves x (16*KJ) keys of one (b, h) (keys on the MFMA lane axis); query tiles of
 // 64 stream through a STG-stage LDS ring filled directly from global memory: per tile the Q row image, the Q
 // transposed-read image, the dO row image, the dO transposed-read image (8 pieces of 8 rows x 128 B each, 8 per wave)
@@ -677,14 +931,21 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // workgroups, else 128 (4 x 32): fewer K/V LDS bytes per MFMA vs. a fuller grid
   const int nq4 = cdiv(Sq, 256), nq2 = cdiv(Sq, 128);
   // cross-attention (77 keys: two key tiles) keeps 128: its per-workgroup set-up outweighs the K/V reuse (-10 %)
-  const bool big = g_attn_fwd_variant == 4 || (g_attn_fwd_variant == 0 && (long)nq4 * H * B >= 1024 && Sk > 128);
+  // fwd variant knob (benchmarks only): 0 auto, 2 / 4 force 32 / 64 rows per wave, +5 (5, 7, 9) the first-round loop
+  const int fv = g_attn_fwd_variant;
+  const int qsel = fv >= 5 ? fv - 5 : fv;
+  const bool big = qsel == 4 || (qsel == 0 && (long)nq4 * H * B >= 1024 && Sk > 128);
+  hipStream_t st = (hipStream_t)stream;
   if (g_attn_vsum) {
-    if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
-    else attn_fwd_kernel<2, false><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
+    if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
+    else attn_fwd_kernel<2, false><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
+  } else if (fv >= 5) {
+    if (big) attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
+    else attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
   } else if (big) {
-    attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq4);
+    attn_fwd2_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
   } else {
-    attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, (hipStream_t)stream>>>(a, nq2);
+    attn_fwd2_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
   }
   return pso_check_launch("pso_attention_fwd");
 }

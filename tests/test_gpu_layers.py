@@ -114,6 +114,39 @@ def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("variant", [2, 4, 7, 9])  # 2 / 4: deferred-rescale forward, 32 / 64 rows per wave; 7 / 9: first-round loop
+@pytest.mark.parametrize("case", ["ramp", "spike"])
+def test_attention_fwd_rescale_paths(cuda, variant, case):
+    """The forward's deferred rescale: keys scaled up along the sequence make every row's max creep up tile after
+    tile (growth below the threshold: P exceeds 1 and the rescale is skipped), a late spike key makes some rows' max
+    jump by far more than the threshold after 60 tiles (the rescale fires with O, l and the max all moving)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    B, H, Sq, Sk = 1, 2, 512, 4096
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(11)
+    q = torch.randn(B, Sq, C, device=cuda, generator=g)
+    k = torch.randn(B, Sk, C, device=cuda, generator=g)
+    v = torch.randn(B, Sk, C, device=cuda, generator=g)
+    if case == "ramp":
+        k = k * torch.linspace(0.5, 3.0, Sk, device=cuda)[None, :, None]
+    else:
+        k[:, Sk - 70] = 2.0 * q[:, 5]      # query 5 (and its neighbours by chance) meets a key ~20 log2 units up
+        k[:, Sk - 3] = -1.5 * q[:, 300]
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    K.lib().pso_attention_set_variant(variant)
+    try:
+        o, lse = K.attention_fwd(q, k, v, H)
+    finally:
+        K.lib().pso_attention_set_variant(0)
+    ref = _attn_ref(q, k, v, H)
+    f = lambda t: t.float().reshape(B, t.shape[1], H, 64).transpose(1, 2)
+    ref_lse = torch.logsumexp(f(q) @ f(k).transpose(-1, -2) * 0.125, dim=-1)
+    assert _rel(o, ref) < 1e-2
+    assert (lse - ref_lse).abs().max().item() < 2e-3 * max(1.0, ref_lse.abs().max().item() / 8)
+    # row-wise: the spiked rows are dominated by one key, so their output is that key's value row
+    assert (o.float() - ref).abs().max().item() < 0.06
+
+
 @pytest.mark.parametrize("variant", [0, 32])  # 0: 2-phase 256x256 kernel; 32: the 8-phase kernel where K % 128 == 0
 @pytest.mark.parametrize("M,dim", [(8192, 1280), (300, 64), (1000, 640)])
 def test_gemm_geglu_fused(cuda, M, dim, variant):
