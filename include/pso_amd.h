@@ -124,6 +124,13 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
              int tail_group_n, int tail_rows, void* stream);
 
+/* Batched dense product out_z[M][N] = alpha * A_z[M][K] . B_z[N][K]^T for z < batch, operand z at z * stride_* elements
+ * (bf16 A/B, bf16 or f32 out).  Replaces the per-image loop of the VAE mid-block attention (diffusers Attention with
+ * one 512-wide head over the H*W tokens, AutoencoderKL decode at DP/sdxl_turbo_with_logprob.py:154-155): scores
+ * S_z = Q_z K_z^T and O_z = P_z V_z for every image of the batch in one launch each. */
+int pso_gemm_batched(int batch, int M, int N, int K, const void* a, long lda, long stride_a, const void* b, long ldb,
+                     long stride_b, float alpha, void* out, long ldo, long stride_o, int out_dtype, void* stream);
+
 /* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
  * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
  * 6 = 64x128 (4 waves), 7 = 128x256 (8 waves), 8 = 128x128 (8 waves). */

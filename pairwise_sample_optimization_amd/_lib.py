@@ -44,6 +44,7 @@ SIGNATURES = {
     "pso_db_loss_bwd": (ci, [ci, ci, ci, vp, ci, vp, vp, vp, cf, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, ci, vp]),
+    "pso_gemm_batched": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
     "pso_gemm8p_skip_epilogue": (None, [ci]),
     "pso_gemm_tn_set_split": (None, [ci]),

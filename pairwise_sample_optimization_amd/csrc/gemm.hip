@@ -54,6 +54,9 @@ struct GemmArgs {
   // writes the interleaved input gradient [dout*gelu(g) | dout*h*gelu'(g)] to out (2N columns).
   void* out2; long ldo2;
   const bf16_t* aux; long ldaux;
+  // batched form (gridDim.z = batch, dense A only): operand z starts batch strides further on (elements)
+  long bat_a, bat_b, bat_o;
+  int batch;
 };
 
 #define EPI_NONE 0
@@ -198,8 +201,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   const int prow = lane >> 3;
   const int pch = lane & 7;
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero16);
-  const bf16_t* const a1 = g.a1;
-  const bf16_t* const b1 = g.b1;
+  const long zb = blockIdx.z;
+  const bf16_t* const a1 = g.a1 + zb * g.bat_a;
+  const bf16_t* const b1 = g.b1 + zb * g.bat_b;
+  void* const outp = reinterpret_cast<char*>(g.out) + zb * g.bat_o * (g.out_dtype == PSO_F32 ? 4 : 2);
   const int K1 = g.K1;
   int lcA[T::A_CH], offA[T::A_CH];  // logical chunk (source-side swizzle) and element offset of this lane's rows
   int lcB[T::B_CH], offB[T::B_CH];
@@ -462,7 +467,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(vh[0], vh[1]), pack2bf(vh[2], vh[3]));
           *reinterpret_cast<uint2*>(p + 32) = make_uint2(pack2bf(vg[0], vg[1]), pack2bf(vg[2], vg[3]));
         }
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ng / 2 + jj * 16 + fk * 4) =
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(outp) + (long)m * g.ldo + ng / 2 + jj * 16 + fk * 4) =
             make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
       }
     }
@@ -528,7 +533,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           oh[e] = pack2bf(d0 * g0 * c0, d1 * g1 * c1);
           og[e] = pack2bf(d0 * h0 * (c0 + 0.39894228040143268f * g0 * e0), d1 * h1 * (c1 + 0.39894228040143268f * g1 * e1));
         }
-        bf16_t* p = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
+        bf16_t* p = reinterpret_cast<bf16_t*>(outp) + (long)m * g.ldo + ph;
         *reinterpret_cast<uint4*>(p) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
         *reinterpret_cast<uint4*>(p + 32) = make_uint4(og[0], og[1], og[2], og[3]);
       }
@@ -605,7 +610,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
             o[e] = pack2bf(bf2f(yw[e] & 0xffff) + bf2f(rw[e] & 0xffff), bf2f(yw[e] >> 16) + bf2f(rw[e] >> 16));
           y = make_uint4(o[0], o[1], o[2], o[3]);
         }
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + cl) = y;
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(outp) + (long)m * g.ldo + n0 + cl) = y;
       }
       return;
     }
@@ -628,10 +633,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           v[2] += bf2f(eadd[i][j].y & 0xffff); v[3] += bf2f(eadd[i][j].y >> 16);
         }
         if (g.out_dtype == PSO_BF16) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(outp) + (long)m * g.ldo + n) =
               make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
         } else {
-          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n);
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(outp) + (long)m * g.ldo + n);
           if (g.accumulate) {
             const float4 old = *o;
             v[0] += old.x; v[1] += old.y; v[2] += old.z; v[3] += old.w;
@@ -653,7 +658,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       float v[4] = {acc[i][j][0] * g.alpha, acc[i][j][1] * g.alpha, acc[i][j][2] * g.alpha,
                     acc[i][j][3] * g.alpha};
       if (gridDim.y > 1) {  // split-K partial: f32 accumulate output, no bias / residual (host-checked)
-        float* o = reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n;
+        float* o = reinterpret_cast<float*>(outp) + (long)m * g.ldo + n;
         for (int r = 0; r < 4 && n + r < g.N; ++r) atomicAdd(o + r, v[r]);
         continue;
       }
@@ -672,10 +677,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           v[0] += bf2f(rv.x & 0xffff); v[1] += bf2f(rv.x >> 16); v[2] += bf2f(rv.y & 0xffff); v[3] += bf2f(rv.y >> 16);
         }
         if (g.out_dtype == PSO_BF16) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n) =
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(outp) + (long)m * g.ldo + n) =
               make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
         } else {
-          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n);
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(outp) + (long)m * g.ldo + n);
           if (g.accumulate) {
             const float4 old = *o;
             v[0] += old.x; v[1] += old.y; v[2] += old.z; v[3] += old.w;
@@ -689,9 +694,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
           if (g.rowbias) x += bf2f(g.rowbias[(long)(m / g.rows_per_group) * g.ld_rowbias + n + r]);
           if (g.resid) x += bf2f(g.resid[(long)m * g.ldr + n + r]);
           if (g.out_dtype == PSO_BF16) {
-            reinterpret_cast<bf16_t*>(g.out)[(long)m * g.ldo + n + r] = f2bf(x);
+            reinterpret_cast<bf16_t*>(outp)[(long)m * g.ldo + n + r] = f2bf(x);
           } else {
-            float* o = reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n + r;
+            float* o = reinterpret_cast<float*>(outp) + (long)m * g.ldo + n + r;
             *o = g.accumulate ? *o + x : x;
           }
         }
@@ -703,7 +708,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
 template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 2, bool PIPE = false, int EPI = EPI_NONE>
 static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   const int nblk = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  dim3 grid(nblk, ksplit);
+  dim3 grid(nblk, ksplit, g.batch > 1 ? g.batch : 1);
   const int threads = 64 * WM * WN;
   const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
   static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
@@ -780,6 +785,12 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const bool bn64_only = g.tail_group_n > 0 && (g.tail_group_n % 128) != 0;  // grouped tail needs BN | group
   const bool bn256_ok = g.tail_group_n == 0 || (g.tail_group_n % 256) == 0;
   const long Ktot = (long)g.K1 + (g.a2 ? g.K2 : 0);
+  if (g.batch > 1) {  // batched dense product (the VAE's single-head mid attention): the 2-phase tiles only
+    auto tl = [&](int bm, int bn) { return (long)((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn) * g.batch; };
+    if ((g.N % 160) == 0 && tl(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
+    if (tl(128, 128) >= 256) return launch<128, 128, 2, 4, 2>(g, st);
+    return launch<64, 64>(g, st);
+  }
   // Skinny N (the LoRA rank-r products): one 16-row x all-N tile per 4-wave block, K split over the waves.
   if (gv == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
       (g.N % 4) == 0 && g.vec_ok && g.M >= 256)
@@ -796,10 +807,10 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if (ks < 1) ks = 1;
     return launch<64, 64>(g, st, (int)ks);
   }
-  // 8-phase 256x256 (gemm8p.hip) for dense bf16 GEMMs with N % 256 == 0: LDS-staged 16-B epilogue, LoRA K-tail,
-  // bias / alpha / residual.  Opt-in (variant 30 / 32): inside the C2 step it measured equal to the 2-phase kernels on
-  // the q/k/v projection (983 vs 971 TF/s, 16384 x 3840 x 1280 + tail) while the GEMM that follows it slowed down by
-  // about what it saved (its output's dirty lines are written back during the next kernel), tools/shape_prof.py.
+  // 8-phase 256x256 (gemm8p.hip, wave groups staggered) for dense bf16 GEMMs with N % 256 == 0: LDS-staged 16-B
+  // epilogue, LoRA K-tail, bias / alpha / residual.  Default for N >= 2560 with >= 256 tiles (tools/gemm8_ab.py, one
+  // box: q/k/v 16384 x 3840 x 1280 1071 vs 937 TF/s, ff.out dX 8192 x 5120 x 1280 991 vs 945); N = 1280 keeps 128x160
+  // (1.25 rounds of 256x256 tiles at M = 16384: 805 vs 928).  Variant 30 forces it, 31 keeps it off everywhere.
   const bool ok8 = !g.conv.mode && !g.rowbias && g.out_dtype == PSO_BF16 && !g.accumulate && (g.N % 256) == 0 &&
                    (g.K1 % 64) == 0 && al16(g.a1) && al16(g.b1) && (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 &&
                    al16(g.out) && (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
@@ -807,7 +818,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
                    (!g.a2 || ((g.tail_group_n == 0 || (g.tail_group_n % 256) == 0) && fits30(g.tail_m, g.lda2) &&
                               fits30(g.N, g.ldb2)));
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
-  if (ok8 && (gv == 30 || (gv == 32 && t256 >= 256)))
+  if (ok8 && (gv == 30 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);
@@ -997,6 +1008,25 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
   g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  return run_gemm(g, (hipStream_t)stream);
+}
+
+int pso_gemm_batched(int batch, int M, int N, int K, const void* a, long lda, long stride_a, const void* b, long ldb,
+                     long stride_b, float alpha, void* out, long ldo, long stride_o, int out_dtype, void* stream) {
+  PSO_ARG_CHECK(batch >= 1 && M >= 0 && N >= 0 && K >= 0 && (K % 8) == 0, "pso_gemm_batched: bad shape (K %% 8 == 0)");
+  PSO_ARG_CHECK(a && b && out, "pso_gemm_batched: null operand");
+  PSO_ARG_CHECK(al16(a) && al16(b) && (lda % 8) == 0 && (ldb % 8) == 0 && (stride_a % 8) == 0 && (stride_b % 8) == 0,
+                "pso_gemm_batched: A/B need 16-B aligned rows and batch strides");
+  PSO_ARG_CHECK(out_dtype == PSO_BF16 || out_dtype == PSO_F32, "pso_gemm_batched: bad out dtype");
+  PSO_ARG_CHECK((long)M * lda < 0x7fffffffL && (long)N * ldb < 0x7fffffffL,
+                "pso_gemm_batched: one operand spans more than 2^31 elements");
+  GemmArgs g{};
+  g.a1 = (const bf16_t*)a; g.lda1 = lda; g.K1 = K;
+  g.b1 = (const bf16_t*)b; g.ldb1 = ldb;
+  g.M = M; g.N = N; g.tail_m = M;
+  g.alpha = alpha; g.rows_per_group = 1;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype;
+  g.bat_a = stride_a; g.bat_b = stride_b; g.bat_o = stride_o; g.batch = batch;
   return run_gemm(g, (hipStream_t)stream);
 }
 

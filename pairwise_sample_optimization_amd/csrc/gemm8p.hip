@@ -55,7 +55,12 @@ constexpr int HT = 128 * 64;  // elements of one half-tile image [128 rows][64 k
 
 __device__ __forceinline__ int swz8(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
 
-template <int EPI>
+// STAG: the two wave groups (waves 0-3 / 4-7, one of each per SIMD) run half a phase apart -- waves 4-7 take one
+// extra s_barrier before the main loop, waves 0-3 one after it -- so on every SIMD one wave's MFMA segment runs beside
+// its partner's fragment-read / staging segment (ping-pong).  Every phase then retires its own fragment reads
+// (lgkmcnt(0)) before its first barrier: with the lag, a partner may restage an image one barrier after that point.
+// SPRIO: waves 4-7 hold s_setprio 1 for the whole main loop instead of every wave raising it around its MFMAs.
+template <int EPI, bool STAG, bool SPRIO>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1][HT]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     }
   };
   auto mfma_q = [&](int ha, int hb) {
-    __builtin_amdgcn_s_setprio(1);
+    if (!SPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[ha][hb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (!SPRIO) __builtin_amdgcn_s_setprio(0);
   };
   // one phase: reads (RA / RB: which operand image to (re)load), the stage (if its K-tile exists), the optional
   // counted wait (VM: -1 none, else vmcnt(VM)), barrier, MFMAs of quadrant (HA, HB), barrier.
@@ -205,6 +210,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     if (RB) read_b((BUF) * 4 + 2 + (HB));                                                     \
     if (RA) read_a((BUF) * 4 + (HA));                                                         \
     if ((STAGE_KT) < nt) stage((STAGE_KT), (STAGE_IMG));                                      \
+    if (STAG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
     if ((VM) == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");                           \
     else if ((VM) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                      \
     __builtin_amdgcn_s_barrier();                                                             \
@@ -220,6 +226,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   if (nt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if (STAG && wave >= 4) __builtin_amdgcn_s_barrier();
+  if (SPRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   for (int j = 0; j < nt; j += 2) {
     const bool last = j + 2 >= nt;
@@ -237,6 +245,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     else { PHASE(1, 0, 1, 1, 0, j + 3, 7, -1) }
   }
 #undef PHASE
+  if (STAG && wave < 4) __builtin_amdgcn_s_barrier();
+  if (SPRIO) __builtin_amdgcn_s_setprio(0);
 
   // ---- epilogue: lane holds out[m = m0 + 128 ha + 32 wr + 16 i + fr][n = n0 + 128 hb + 64 wc + 16 j + 4 fk + r] ----
   if (g.skip_epi) {
@@ -367,17 +377,28 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   }
 }
 
-template <int EPI>
+template <int EPI, bool STAG, bool SPRIO>
 int launch8(const Gemm8Args& g, hipStream_t st) {
   const int nblk = ((g.M + 255) / 256) * (g.N / 256);
   const size_t shm = 8 * HT * sizeof(bf16_t);  // 128 KiB
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
     attr_done = true;
   }
-  gemm8p_kernel<EPI><<<nblk, 512, shm, st>>>(g);
+  gemm8p_kernel<EPI, STAG, SPRIO><<<nblk, 512, shm, st>>>(g);
   return pso_check_launch("pso_gemm(8-phase)");
+}
+
+template <int EPI>
+int launch8s(const Gemm8Args& g, hipStream_t st, int mode) {
+  switch (mode & 3) {
+    case 0: return launch8<EPI, true, false>(g, st);
+    case 1: return launch8<EPI, false, false>(g, st);
+    case 2: return launch8<EPI, true, true>(g, st);
+    default: return launch8<EPI, false, true>(g, st);
+  }
 }
 
 }  // namespace
@@ -385,7 +406,10 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
 // Host entries used by gemm.hip (preconditions checked there): N % 256 == 0, K % 64 == 0, 16-B aligned rows, every
 // operand's M * ld (or N * ld) below 2^30 elements (byte offsets of the buffer loads are 32-bit).
 static int g_skip_epi8 = 0;
-extern "C" void pso_gemm8p_skip_epilogue(int on) { g_skip_epi8 = on; }
+// benchmark knobs, bit 1: wave groups in lockstep (default: staggered by half a phase, +10-18 % on every UNet shape,
+// tools/gemm8_ab.py); bit 2: static priority for waves 4-7
+static int g_mode8 = 0;
+extern "C" void pso_gemm8p_skip_epilogue(int on) { g_skip_epi8 = on & 1; g_mode8 = (on >> 1) & 3; }
 
 int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2,
                    long lda2, int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha,
@@ -400,7 +424,7 @@ int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const 
   g.out = out; g.ldo = ldo; g.out2 = out2; g.ldo2 = ldo2; g.pre_rows = pre_rows;
   g.aux = (const bf16_t*)aux; g.ldaux = ldaux;
   g.group_m = group_m; g.skip_epi = g_skip_epi8;
-  if (epi == EPI8_GEGLU) return launch8<EPI8_GEGLU>(g, st);
-  if (epi == EPI8_GEGLU_BWD) return launch8<EPI8_GEGLU_BWD>(g, st);
-  return launch8<EPI8_NONE>(g, st);
+  if (epi == EPI8_GEGLU) return launch8s<EPI8_GEGLU>(g, st, g_mode8);
+  if (epi == EPI8_GEGLU_BWD) return launch8s<EPI8_GEGLU_BWD>(g, st, g_mode8);
+  return launch8s<EPI8_NONE>(g, st, g_mode8);
 }

@@ -103,6 +103,25 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
     return out
 
 
+def gemm_batched(a, w, alpha=1.0, out=None, out_dtype=BF16):
+    """out[z] = alpha * a[z] @ w[z]^T for a [Z, M, K], w [Z, N, K] (bf16, rows contiguous) -> [Z, M, N]."""
+    require_cuda(a, w)
+    Z, M, Kd = a.shape
+    N = w.shape[1]
+    assert w.shape[0] == Z and w.shape[2] == Kd and a.dtype == BF16 and w.dtype == BF16
+    assert a.stride(2) == 1 and w.stride(2) == 1
+    if out is None:
+        out = torch.empty((Z, M, N), device=a.device, dtype=out_dtype)
+    assert out.stride(2) == 1 and tuple(out.shape) == (Z, M, N)
+    e0 = _prof_begin()
+    check(lib().pso_gemm_batched(Z, M, N, Kd, ptr(a), a.stride(1), a.stride(0), ptr(w), w.stride(1), w.stride(0),
+                                 float(alpha), ptr(out), out.stride(1), out.stride(0), dtype_code(out), stream_ptr()),
+          "pso_gemm_batched")
+    _prof_end(e0, 2.0 * Z * M * N * Kd, 2.0 * Z * (M * Kd + N * Kd) + out.element_size() * Z * M * N,
+              ("gemm_batched", Z, M, N, Kd))
+    return out
+
+
 def gemm_grouped_skinny(a, w, groups, out=None, alpha=1.0):
     """Block-diagonal skinny product: out[:, g*N:(g+1)*N] = alpha * a[:, g*K:(g+1)*K] @ w[:, g*K:(g+1)*K]^T, bf16."""
     M, KG = a.shape
@@ -655,6 +674,15 @@ class BatchedTranspose:
         if self.n:
             check(lib().pso_transpose_batched(self.n, ptr(self.desc), self.max_r, self.max_c, stream_ptr()),
                   "pso_transpose_batched")
+
+
+def transpose_batched(x, out=None):
+    """[Z, R, C] (rows contiguous) -> [Z, C, R] bf16 in one launch (a descriptor per matrix)."""
+    Z, R, C = x.shape
+    if out is None:
+        out = torch.empty((Z, C, R), device=x.device, dtype=x.dtype)
+    BatchedTranspose([(x[z], out[z]) for z in range(Z)], x.device)()
+    return out
 
 
 def gather_rows(src, idx, out=None):

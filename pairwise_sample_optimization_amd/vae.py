@@ -9,7 +9,8 @@ each; channels 512,512,256,128; nearest-2x upsample + conv on the first three) -
 GroupNorm eps 1e-6, 32 groups, no time embedding.
 
 All activations NHWC bf16.  The mid-block attention has head dim 512 (outside the d=64 flash kernel); its 16384 x 16384
-score matrix per image is small next to 288 GB, so it runs as GEMM (scores, bf16) -> row softmax -> GEMM.
+score matrix per image is small next to 288 GB, so it runs as one batched GEMM (scores, bf16, every image) -> row
+softmax -> one batched GEMM.
 
 The encoder (the DreamBooth PSO step's `vae.encode(pixel_values).latent_dist.sample()`, DB:1750) is
 restated from diffusers 0.27.0 Encoder: conv_in (3->128) -> 4 DownEncoderBlock2D (2 resnets each; channels
@@ -61,15 +62,15 @@ class VAEAttention(nn.Module):
         S = H * W
         hn, _ = K.group_norm_fwd(x, self.group_norm.weight, self.group_norm.bias, self.groups, 1e-6, False)
         qkv = K.gemm(hn.view(-1, C), self.w_qkv, bias=self.b_qkv).view(B, S, 3 * C)
-        out = torch.empty((B * S, C), device=x.device, dtype=BF16)
         scale = 1.0 / math.sqrt(C)
-        for b in range(B):  # per image: S x S scores stay well under HBM
-            q, k, v = qkv[b, :, :C], qkv[b, :, C:2 * C], qkv[b, :, 2 * C:]
-            s = K.gemm(q, k, alpha=scale)
-            K.softmax_rows(s)
-            K.gemm(s, K.transpose(v), out=out[b * S:(b + 1) * S])
+        # every image in one launch per product: S_b = Q_b K_b^T (bf16, B x 512 MB at 1024^2), row softmax,
+        # O_b = P_b V_b with V_b transposed once for all images (one batched transpose)
+        s = K.gemm_batched(qkv[:, :, :C], qkv[:, :, C:2 * C], alpha=scale)            # [B, S, S]
+        K.softmax_rows(s.view(B * S, S))
+        vt = K.transpose_batched(qkv[:, :, 2 * C:])                                    # [B, C, S]
+        out = K.gemm_batched(s, vt)                                                    # [B, S, C]
         o = self.to_out[0]
-        return K.gemm(out, o.weight, bias=o.bias, resid=x.view(-1, C)).view(B, H, W, C)
+        return K.gemm(out.view(B * S, C), o.weight, bias=o.bias, resid=x.view(-1, C)).view(B, H, W, C)
 
 
 class _Blk(nn.Module):

@@ -26,6 +26,28 @@ def test_gemm_vs_fp32(cuda, M, N, K):
     assert _rel(out32, a.float() @ w.float().t()) < 1e-5
 
 
+@pytest.mark.parametrize("Z,M,N,K", [(3, 1024, 1024, 512), (2, 4096, 512, 4096), (4, 200, 96, 64), (1, 300, 160, 512)])
+def test_gemm_batched_vs_fp32(cuda, Z, M, N, K):
+    """The batched product of the VAE mid attention (scores Q K^T, then P V^T-operand) against torch.bmm in fp32."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(Z * 131 + M + N)
+    a = torch.randn(Z, M, K, device=cuda, generator=g).bfloat16()
+    w = (torch.randn(Z, N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    ref = torch.bmm(a.float(), w.float().transpose(1, 2))
+    out = K_.gemm_batched(a, w, alpha=0.25)
+    assert _rel(out, 0.25 * ref) < 4e-3
+    out32 = K_.gemm_batched(a, w, out_dtype=torch.float32)
+    assert _rel(out32, ref) < 1e-5
+    for z in range(Z):  # no batch entry bleeds into another
+        assert _rel(out32[z], ref[z]) < 1e-5
+    # strided views (the VAE passes column slices of the fused qkv rows)
+    qkv = torch.randn(Z, M, 3 * K, device=cuda, generator=g).bfloat16()
+    o2 = K_.gemm_batched(qkv[:, :, :K], qkv[:, :N, K:2 * K], out_dtype=torch.float32)
+    assert _rel(o2, torch.bmm(qkv[:, :, :K].float(), qkv[:, :N, K:2 * K].float().transpose(1, 2))) < 1e-5
+    t = K_.transpose_batched(a)
+    assert torch.equal(t, a.transpose(1, 2))
+
+
 def test_gemm_lora_tail_and_accumulate(cuda):
     from pairwise_sample_optimization_amd import kernels as K_
     M, N, K, r = 640, 640, 640, 32
