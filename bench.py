@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--num-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--epochs", type=int, default=2,
+                    help="timed full epochs (sampling + VAE decode + PickScore + training) for the secondary metric; "
+                         "0 skips it")
     ap.add_argument("--graph", action="store_true",
                     help="replay each epoch as one captured hipGraph (measured neutral: 31.32 vs 31.36 imgs/s eager)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -155,6 +158,61 @@ def cpu_baseline(args, unet):
                       f"{dt:.1f} s"}
 
 
+SDXL_FWD_TFLOP_PER_IMG = 6.765   # one UNet forward at 1024^2
+VAE_DEC_TFLOP_PER_IMG = 10.49    # AutoencoderKL.decode at 1024^2
+
+
+def epoch_metric(args, dev, tr, buf, g, n_epochs):
+    """Secondary metric (SURVEY §8d "epoch imgs/s"): one full online epoch = paired sampling of P*gas prompts (N UNet
+    forwards over both trajectories of every prompt, batched) -> VAE decode of the final latents -> PickScore reward
+    (ViT-H/14 on the GPU-preprocessed images; random-init weights, random prompt ids) -> shuffle -> training epoch
+    (the timed step above).  value = trained images / wall time of the whole epoch."""
+    from pairwise_sample_optimization_amd.vae import AutoencoderKL, VAEConfig
+    from pairwise_sample_optimization_amd.pso_pytorch.pickscore_utils import Selector
+    from pairwise_sample_optimization_amd.rewards import pickscore_reward
+    h = args.res // 8
+    with torch.device(dev):
+        vae = AutoencoderKL(VAEConfig())
+    vae.init_weights(0)
+    vae.prepare()
+    sel = Selector(dev, seed=0)
+    Bp = args.pairs * args.gas
+    ids = torch.randint(1, 49406, (Bp, 77), device=dev, generator=g)
+    ids[:, 0], ids[:, 20:] = 49406, 49407
+    reward = pickscore_reward(sel, ids.repeat_interleave(2, 0))
+    enc, pooled, tid = buf["enc"][::2].contiguous(), buf["pooled"][::2].contiguous(), buf["tid"][::2].contiguous()
+
+    def epoch():
+        b = tr.sample_pairs(enc, pooled, tid, h, generator=g, reward_fn=reward, decode_fn=vae.decode_latents_nhwc)
+        one_step(tr, b, g)
+
+    epoch()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n_epochs):
+        epoch()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dev) / n_epochs
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    n_img = 2 * Bp
+    trained = n_img * (args.num_steps - 1)
+    tf = None
+    if args.res == 1024 and not args.full_unet and args.rank in SURVEY_TFLOP_PER_PAIR_MICRO:
+        tf = (args.num_steps * n_img * SDXL_FWD_TFLOP_PER_IMG + n_img * VAE_DEC_TFLOP_PER_IMG
+              + SURVEY_TFLOP_PER_PAIR_MICRO[args.rank] * Bp * (args.num_steps - 1))
+    out = {"imgs_per_s": round(trained * world / dt, 3), "ms_per_epoch": round(dt * 1e3, 1), "epochs": n_epochs,
+           "sampled_images": n_img * world, "reward": "PickScore ViT-H/14 (random-init weights, random prompt ids)"}
+    if tf:
+        out["tflop_per_epoch_per_gpu"] = round(tf, 1)
+        out["mfma_frac"] = round(tf / dt / PEAK_BF16_TFLOPS, 4)
+    del vae, sel
+    return out
+
+
 def max_over_ranks(dt, dev):
     """The slowest rank sets the job time (barrier-bracketed timed region, MAX over ranks)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -242,6 +300,9 @@ def main():
         res["step_mfma_frac"] = round(step_tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)
     if not args.no_roofline:
         res["roofline"] = roofline(tr, buf, g)
+    if args.epochs > 0:
+        log("[bench] epoch metric ...")
+        res["epoch"] = epoch_metric(args, dev, tr, buf, g, args.epochs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline ...")
         res["cpu_baseline"] = cpu_baseline(args, unet)

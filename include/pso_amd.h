@@ -34,6 +34,7 @@ extern "C" {
 /* dtype codes */
 #define PSO_F32 0
 #define PSO_BF16 1
+#define PSO_U8 2 /* uint8 images (pso_clip_preprocess only) */
 
 /* step modes */
 #define PSO_MODE_TURBO 0 /* Euler-ancestral (SDXL-Turbo)   DP/turbo_inference_with_logprob.py:24-116 */
@@ -318,6 +319,44 @@ int pso_adamw_step(long n, float* param, const float* grad, float* exp_avg, floa
 int pso_zero_f32(long n, float* x, void* stream);
 int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * CLIP towers and the reward image path (clip.hip): the SDXL prompt encoders (CLIP ViT-L/14 text
+ * + OpenCLIP ViT-bigG/14 text, `encode_prompt` T:81-118) and the PickScore reward (CLIP ViT-H/14,
+ * pso_pytorch/pickscore_utils.py:12-62) run their projections on pso_gemm and their norms on pso_layer_norm_fwd;
+ * these are the remaining pieces.
+ * ------------------------------------------------------------------------------------------------------------- */
+#define PSO_ACT_GELU 0       /* exact (erf) GELU: OpenCLIP bigG / ViT-H towers                                    */
+#define PSO_ACT_QUICK_GELU 1 /* x * sigmoid(1.702 x): OpenAI CLIP ViT-L/14 text encoder                          */
+
+/* Softmax attention over short sequences (S <= a few hundred; head dim D <= 128), fp32 online softmax.  Token rows
+ * of q / k / v / o are strided (ld*) inside a batch (stride s*_b); head h occupies columns [h*D, (h+1)*D).  causal:
+ * key j > query i masked (the CLIP text encoders' causal mask). */
+int pso_attention_small(int B, int H, int S, int D, const void* q, long ldq, long sq_b, const void* k, long ldk,
+                        long sk_b, const void* v, long ldv, long sv_b, int causal, float scale, void* o, long ldo,
+                        long so_b, void* stream);
+/* In-place activation of n bf16 values (mode PSO_ACT_*). */
+int pso_activation(long n, void* x, int mode, void* stream);
+/* out[b*S + t][:] = tok[ids[b*S + t]][:] + pos[t][:] (bf16 tables, int64 ids). */
+int pso_embed_tokens(int B, int S, int C, const int64_t* ids, const void* tok, const void* pos, void* out,
+                     void* stream);
+/* Vision embeddings: row 0 of image b = cls + pos[0], row 1 + p = patch[b*P + p] + pos[1 + p]  -> [B*(P+1)][C]. */
+int pso_embed_vision(int B, int P, int C, const void* patch, const void* cls, const void* pos, void* out,
+                     void* stream);
+/* out[i] = cos(a_i, b_i) for fp32 rows (PickScore: diag(text_n @ image_n^T), pickscore_utils.py:50-58). */
+int pso_cosine_rows(int n, int C, const float* a, long lda, const float* b, long ldb, float* out, void* stream);
+/* out[r] = mean of row r (n bf16 values, 16-B aligned rows, n % 8 == 0): light_reward (pso_pytorch/rewards.py:5-9). */
+int pso_row_mean(int rows, long n, const void* x, float* out, void* stream);
+/* Reward-image preprocessing, GPU-resident replacement of T:632-640 + the CLIPImageProcessor: image NHWC bf16
+ * [B,H,W,3] in [-1,1] -> uint8 as ((x + 1) * 127.5).clamp(0, 255).to(uint8) in bf16 arithmetic -> PIL bicubic resize
+ * of the shortest edge to `size` (8-bit fixed point, horizontal then vertical pass, bit-exact) -> centre crop
+ * size x size -> x / 255 -> (x - mean) / std (float32) -> patch rows [B * (size/patch)^2][kpad] bf16 in
+ * (channel, ky, kx) order (zero columns past 3 * patch^2): the A operand of the patch-embedding GEMM. */
+/* Patch rows of an already processed NCHW fp32 image [B, C, S, S] (same layout as pso_clip_preprocess's output). */
+int pso_patchify(int B, int C, int S, int P, int kpad, const float* x, void* out, void* stream);
+size_t pso_clip_preprocess_ws_bytes(int B, int H, int W, int size);
+int pso_clip_preprocess(int B, int H, int W, const void* img, int img_dtype, int size, int patch, int kpad,
+                        const float* mean, const float* stdv, void* out, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

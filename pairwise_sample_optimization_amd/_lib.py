@@ -46,6 +46,15 @@ SIGNATURES = {
                       ci, ci, vp]),
     "pso_gemm_batched": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
+    "pso_attention_small": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, vp, cl, cl, ci, cf, vp, cl, cl, vp]),
+    "pso_activation": (ci, [cl, vp, ci, vp]),
+    "pso_embed_tokens": (ci, [ci, ci, ci, vp, vp, vp, vp, vp]),
+    "pso_embed_vision": (ci, [ci, ci, ci, vp, vp, vp, vp, vp]),
+    "pso_cosine_rows": (ci, [ci, ci, vp, cl, vp, cl, vp, vp]),
+    "pso_row_mean": (ci, [ci, cl, vp, vp, vp]),
+    "pso_patchify": (ci, [ci, ci, ci, ci, ci, vp, vp, vp]),
+    "pso_clip_preprocess_ws_bytes": (csz, [ci, ci, ci, ci]),
+    "pso_clip_preprocess": (ci, [ci, ci, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, csz, vp]),
     "pso_gemm8p_skip_epilogue": (None, [ci]),
     "pso_gemm_tn_set_split": (None, [ci]),
     "pso_attention_set_variant": (None, [ci]),

@@ -4,6 +4,7 @@ Tensors are plain torch device tensors used as memory; every computation happens
 are channels-last bf16: linear inputs are [tokens, C] (any 2-D row-strided view), images are NHWC [B, H, W, C].
 There is no CPU / eager fallback: a missing library or a host tensor raises PsoLibError.
 """
+import ctypes
 import os
 
 import torch
@@ -692,4 +693,93 @@ def gather_rows(src, idx, out=None):
     out = torch.empty((n,) + tuple(src.shape[1:]), device=src.device, dtype=src.dtype) if out is None else out
     check(lib().pso_gather_rows(n, row_bytes, ptr(src.contiguous()), ptr(idx.to(torch.int64).contiguous()),
                                 ptr(out), stream_ptr()), "pso_gather_rows")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# CLIP towers / reward image path (clip.hip)
+# ---------------------------------------------------------------------------------------------------------------------
+ACT_GELU, ACT_QUICK_GELU = 0, 1  # PSO_ACT_*
+
+
+def attention_small(q, k, v, B, S, H, causal, scale, out=None):
+    """q / k / v token-row views [B*S, H*D] (row-strided, e.g. column slices of a fused qkv) -> o [B*S, H*D] bf16."""
+    require_cuda(q, k, v)
+    HD = q.shape[1]
+    D = HD // H
+    if out is None:
+        out = torch.empty((B * S, HD), device=q.device, dtype=BF16)
+    sq, sk, sv, so = _row_stride(q), _row_stride(k), _row_stride(v), _row_stride(out)
+    check(lib().pso_attention_small(B, H, S, D, ptr(q), sq, S * sq, ptr(k), sk, S * sk, ptr(v), sv, S * sv,
+                                    int(bool(causal)), float(scale), ptr(out), so, S * so, stream_ptr()),
+          "pso_attention_small")
+    return out
+
+
+def activation_(x, mode):
+    assert x.is_contiguous() and x.dtype == BF16
+    check(lib().pso_activation(x.numel(), ptr(x), int(mode), stream_ptr()), "pso_activation")
+    return x
+
+
+def embed_tokens(ids, tok, pos):
+    """ids [B, S] int64 (device) -> [B*S, C] = tok[ids] + pos[:S]."""
+    require_cuda(ids, tok, pos)
+    B, S = ids.shape
+    C = tok.shape[1]
+    out = torch.empty((B * S, C), device=tok.device, dtype=BF16)
+    check(lib().pso_embed_tokens(B, S, C, ptr(ids.contiguous()), ptr(tok), ptr(pos), ptr(out), stream_ptr()),
+          "pso_embed_tokens")
+    return out
+
+
+def embed_vision(patch, cls, pos, B, P):
+    C = patch.shape[1]
+    out = torch.empty((B * (P + 1), C), device=patch.device, dtype=BF16)
+    check(lib().pso_embed_vision(B, P, C, ptr(patch), ptr(cls), ptr(pos), ptr(out), stream_ptr()), "pso_embed_vision")
+    return out
+
+
+def cosine_rows(a, b):
+    """[n, C] fp32 x [n, C] fp32 -> cos(a_i, b_i) [n] fp32."""
+    require_cuda(a, b)
+    n, C = a.shape
+    assert a.dtype == torch.float32 and b.dtype == torch.float32 and b.shape == a.shape
+    out = torch.empty(n, device=a.device, dtype=torch.float32)
+    check(lib().pso_cosine_rows(n, C, ptr(a), _row_stride(a), ptr(b), _row_stride(b), ptr(out), stream_ptr()),
+          "pso_cosine_rows")
+    return out
+
+
+def row_mean(x):
+    """[B, ...] bf16 (contiguous) -> per-row mean [B] fp32."""
+    require_cuda(x)
+    B = x.shape[0]
+    out = torch.empty(B, device=x.device, dtype=torch.float32)
+    check(lib().pso_row_mean(B, x[0].numel(), ptr(x.contiguous()), ptr(out), stream_ptr()), "pso_row_mean")
+    return out
+
+
+def patchify(x, P, kpad):
+    """processed pixel values NCHW [B, C, S, S] -> patch rows [B * (S/P)^2, kpad] bf16."""
+    require_cuda(x)
+    B, C, S, _ = x.shape
+    out = torch.empty((B * (S // P) ** 2, kpad), device=x.device, dtype=BF16)
+    check(lib().pso_patchify(B, C, S, P, kpad, ptr(x.float().contiguous()), ptr(out), stream_ptr()), "pso_patchify")
+    return out
+
+
+def clip_preprocess(img, size, P, kpad, mean, std):
+    """decoded images NHWC [B, H, W, 3] (bf16 / f32 in [-1, 1], or uint8) -> patch rows [B * (size/P)^2, kpad] bf16
+    (uint8 quantisation, PIL bicubic resize, centre crop, rescale, normalise)."""
+    require_cuda(img)
+    B, H, W, C = img.shape
+    assert C == 3 and img.dtype in (BF16, torch.float32, torch.uint8) and img.is_contiguous()
+    ws = torch.empty(lib().pso_clip_preprocess_ws_bytes(B, H, W, size), device=img.device, dtype=torch.uint8)
+    out = torch.empty((B * (size // P) ** 2, kpad), device=img.device, dtype=BF16)
+    m = (ctypes.c_float * 3)(*mean)
+    sd = (ctypes.c_float * 3)(*std)
+    code = 2 if img.dtype == torch.uint8 else dtype_code(img)  # PSO_U8
+    check(lib().pso_clip_preprocess(B, H, W, ptr(img), code, size, P, kpad, m, sd, ptr(out), ptr(ws),
+                                    ws.numel(), stream_ptr()), "pso_clip_preprocess")
     return out

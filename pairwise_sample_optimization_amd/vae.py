@@ -230,9 +230,25 @@ class AutoencoderKL(nn.Module):
         """z NCHW (fp32/bf16) -> image NHWC bf16 [B, 8h, 8w, 3] (values in about [-1, 1], unclamped)."""
         if not self._prepared:
             self.prepare()
-        d = self.decoder
-        B, C, h, w = z.shape
         zp = K.nchw_to_nhwc(z, pad_to=self._lc_pad, scale=scale)                  # [B,h,w,8] (zero-padded C)
+        return self._decode_padded(zp)
+
+    def _decode_padded(self, zp):
+        """Images in chunks whose largest activation ([n, 8h, 8w, 256] at the last upsampler) stays under 2^30
+        elements: the kernels' per-operand 32-bit element offsets (4 images per chunk at 1024^2)."""
+        B, h, w, _ = zp.shape
+        per = max(1, (1 << 30) // (64 * h * w * max(self.cfg.block_out_channels)))
+        if B <= per:
+            return self._decode_chunk(zp)
+        out = torch.empty((B, 8 * h, 8 * w, self.cfg.out_channels), device=zp.device, dtype=BF16)
+        for i in range(0, B, per):  # conv_out writes each chunk's rows of the batch output in place
+            self._decode_chunk(zp[i:i + per], out=out[i:i + per])
+        return out
+
+    def _decode_chunk(self, zp, out=None):
+        d = self.decoder
+        B, h, w, _ = zp.shape
+        C = self.cfg.latent_channels
         pq = K.gemm(zp.view(-1, self._lc_pad), self._pq_w, bias=self.post_quant_conv.bias).view(B, h, w, C)
         cols = K.im2col3(pq, d.conv_in.kp)
         x = K.gemm(cols, d.conv_in.w_col, bias=d.conv_in.bias).view(B, h, w, -1)
@@ -247,7 +263,21 @@ class AutoencoderKL(nn.Module):
                 x = blk.upsamplers[0].fwd(x, rt)
         hn, _ = K.group_norm_fwd(x, d.conv_norm_out.weight, d.conv_norm_out.bias, self.cfg.norm_num_groups, 1e-6,
                                  True)
-        return K.conv2d(hn, d.conv_out.w_nhwc, bias=d.conv_out.bias)
+        return K.conv2d(hn, d.conv_out.w_nhwc, bias=d.conv_out.bias, out=out)
+
+    @torch.no_grad()
+    def decode_latents_nhwc(self, x, scale=None):
+        """Trainer-side decode of the sampler's final latents, kept NHWC: x [B, h, w, C] fp32 (the trajectory buffer
+        layout) -> image NHWC bf16 [B, 8h, 8w, 3].  `vae.decode(latents / scaling_factor)` of
+        DP/sdxl_turbo_with_logprob.py:154-155 (scale defaults to 1 / scaling_factor)."""
+        B, h, w, C = x.shape
+        s = 1.0 / self.cfg.scaling_factor if scale is None else scale
+        # NHWC rows are NCHW images of 1 x 1 pixels: the same pad / scale / cast kernel the NCHW path uses
+        z = x.reshape(B * h * w, C, 1, 1)
+        if not self._prepared:
+            self.prepare()
+        zp = K.nchw_to_nhwc(z, pad_to=self._lc_pad, scale=s).view(B, h, w, self._lc_pad)
+        return self._decode_padded(zp)
 
     @torch.no_grad()
     def encode_nhwc(self, x):
