@@ -102,9 +102,23 @@ def one_step(tr, buf, g, graph=False):
         tr.train_epoch(sb)
 
 
+def src_hash():
+    """Hash of the HIP sources the library is built from: a PMC traffic file is used only for the code it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "pairwise_sample_optimization_amd", "csrc", "*.hip")) +
+                    glob.glob(os.path.join(ROOT, "pairwise_sample_optimization_amd", "csrc", "*.h"))):
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def roofline(tr, buf, g):
-    """One extra profiled step: HIP events around every MFMA GEMM/conv launch (torch's current stream = the launch
-    stream).  achieved = sum of algorithmic 2*M*N*K over those launches / sum of their durations."""
+    """One extra profiled step with HIP events around every GEMM-family launch (on torch's current stream = the
+    launch stream), grouped by the launched kernel (pso_last_kernel).  The roofline is the DOMINANT kernel's (most
+    time per step): achieved = its algorithmic 2*M*N*K flop per launch / its average launch duration.  The whole
+    family is reported beside it.  traffic = HBM bytes per launch of that kernel from the two PMC passes
+    (tools/gpu_full.sh -> tools/parse_prof.py), used only when they were collected on these exact sources."""
+    from collections import defaultdict
     from pairwise_sample_optimization_amd import kernels as K
     K.PROFILE = []
     side, K.SideStream.enabled = K.SideStream.enabled, False  # serial launches: each event pair times one kernel alone
@@ -112,24 +126,35 @@ def roofline(tr, buf, g):
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
     K.SideStream.enabled = side
-    fl = sum(r[0] for r in rec)
-    nb = sum(r[1] for r in rec)
-    ms = sum(r[2].elapsed_time(r[3]) for r in rec)
-    n = len(rec)
+    per = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # kernel -> launches, flop, bytes, ms
+    for fl, nb, e0, e1, _tag, kname in rec:
+        a = per[kname]
+        a[0] += 1
+        a[1] += fl
+        a[2] += nb
+        a[3] += e0.elapsed_time(e1)
+    dom, (n, fl, nb, ms) = max(per.items(), key=lambda kv: kv[1][3])
     achieved = fl / (ms * 1e-3) / 1e12
-    out = {"bound": "mfma", "kernel": "gemm_bf16_kernel<...> (incl. GEGLU fwd/bwd epilogues) + gemm_tn_rank_kernel "
-                                      "(every GEMM / implicit-GEMM conv / LoRA dW launch of one train step)",
-           "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "launches_per_step": n,
-           "flop_per_launch": fl / max(n, 1), "bytes_per_launch": nb / max(n, 1),
-           "avg_launch_us": round(ms * 1e3 / max(n, 1), 2)}
-    # HBM bytes per launch from the PMC passes of the same command (tools/gpu_full.sh -> tools/parse_prof.py)
-    tp = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
-    if tp:
-        t = json.load(open(tp[-1]))
-        out["traffic"] = round(t["traffic_bytes_per_launch"])
-        out["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)"
-        out["traffic_source"] = os.path.relpath(tp[-1], os.path.dirname(os.path.abspath(__file__)))
+    n_all, fl_all, ms_all = len(rec), sum(v[1] for v in per.values()), sum(v[3] for v in per.values())
+    out = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+           "launches_per_step": n, "flop_per_launch": fl / n, "bytes_per_launch": nb / n,
+           "avg_launch_us": round(ms * 1e3 / n, 2), "share_of_family_time": round(ms / ms_all, 3),
+           "family": {"kernels": "every GEMM / implicit-GEMM conv / LoRA rank-product launch of one train step",
+                      "launches_per_step": n_all, "achieved": round(fl_all / (ms_all * 1e-3) / 1e12, 1),
+                      "frac": round(fl_all / (ms_all * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                      "ms_per_step": round(ms_all, 2)}}
+    sh = src_hash()
+    for tp in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        t = json.load(open(tp))
+        if t.get("src_hash") == sh and t.get("kernel") == dom:
+            out["traffic"] = round(t["traffic_bytes_per_launch"])
+            out["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE, gfx950 correction)"
+            out["traffic_source"] = os.path.relpath(tp, ROOT)
+            break
+    else:
+        out["traffic_note"] = f"no PMC pass on these sources (src {sh}) for {dom}"
+    out["src_hash"] = sh
     return out
 
 

@@ -132,6 +132,10 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
 int pso_gemm_batched(int batch, int M, int N, int K, const void* a, long lda, long stride_a, const void* b, long ldb,
                      long stride_b, float alpha, void* out, long ldo, long stride_o, int out_dtype, void* stream);
 
+/* Name of the last GEMM-family kernel this thread launched, as rocprofv3 prints it (e.g.
+ * "gemm_bf16_kernel<128, 160, 0, 2, 2, 2, false, 0>"): lets the bench attribute its HIP-event timings per kernel. */
+const char* pso_last_kernel(void);
+
 /* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
  * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
  * 6 = 64x128 (4 waves), 7 = 128x256 (8 waves), 8 = 128x128 (8 waves). */

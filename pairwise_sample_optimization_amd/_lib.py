@@ -46,6 +46,7 @@ SIGNATURES = {
                       ci, ci, vp]),
     "pso_gemm_batched": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
+    "pso_last_kernel": (ctypes.c_char_p, []),
     "pso_attention_small": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, vp, cl, cl, ci, cf, vp, cl, cl, vp]),
     "pso_activation": (ci, [cl, vp, ci, vp]),
     "pso_embed_tokens": (ci, [ci, ci, ci, vp, vp, vp, vp, vp]),

@@ -6,6 +6,14 @@
 #include "common.h"
 
 static thread_local char g_last_error[1024] = "";
+static thread_local char g_last_kernel[160] = "";
+
+void pso_note_kernel(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_kernel, sizeof(g_last_kernel), fmt, ap);
+  va_end(ap);
+}
 
 void pso_set_error(const char* fmt, ...) {
   va_list ap;
@@ -25,5 +33,6 @@ int pso_check_launch(const char* what) {
 
 extern "C" {
 const char* pso_last_error(void) { return g_last_error; }
+const char* pso_last_kernel(void) { return g_last_kernel; }
 int pso_abi_version(void) { return PSO_ABI_VERSION; }
 }

@@ -66,6 +66,10 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
+// ---- launch bookkeeping (host): the demangled name of the last GEMM-family kernel launched on this thread, as
+// rocprofv3 prints it, so HIP-event timings can be attributed per kernel (bench.py roofline) ----
+void pso_note_kernel(const char* fmt, ...);
+
 // ---- error plumbing (host) ----
 void pso_set_error(const char* fmt, ...);
 int pso_check_launch(const char* what);

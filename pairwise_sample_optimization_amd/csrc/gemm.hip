@@ -711,6 +711,8 @@ static int launch(const GemmArgs& g, hipStream_t st, int ksplit = 1) {
   dim3 grid(nblk, ksplit, g.batch > 1 ? g.batch : 1);
   const int threads = 64 * WM * WN;
   const size_t shm = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16_t);
+  pso_note_kernel("gemm_bf16_kernel<%d, %d, %d, %d, %d, %d, %s, %d>", BM, BN, EPI != EPI_NONE ? 0 : g.conv.mode, WM, WN,
+                  STAGES, PIPE ? "true" : "false", EPI);
   static bool attr_done = false;  // >64 KiB dynamic LDS needs the attribute once per instantiation
   if constexpr (EPI != EPI_NONE) {  // fused-activation epilogues: dense operands only
     if (!attr_done) {
@@ -1164,6 +1166,7 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   int ks = g_tn_split > 0 ? g_tn_split : (160 + tiles - 1) / tiles;
   if (ks > nkt) ks = nkt;
   if (ks < 1) ks = 1;
+  pso_note_kernel("gemm_tn_kernel");
   gemm_tn_kernel<<<dim3(tiles, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B,
                                                                    ldb, alpha, out, ldo);
   return pso_check_launch("pso_gemm_tn");

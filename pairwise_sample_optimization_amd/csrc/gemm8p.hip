@@ -387,6 +387,7 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
                               (int)shm);
     attr_done = true;
   }
+  pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
   gemm8p_kernel<EPI, STAG, SPRIO><<<nblk, 512, shm, st>>>(g);
   return pso_check_launch("pso_gemm(8-phase)");
 }

@@ -123,26 +123,32 @@ int launch_skinny(int M, int N, int K, const bf16_t* a, long lda, const bf16_t* 
   const int var = NJ <= 2 ? skinny_variant() : 0;
   if (var == 1 || var == 3) {
     const dim3 grid((M + 15) / 16, groups);
-    if (var == 1)
+    if (var == 1) {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 1, 8);
       gemm_skinny_nt_kernel<NJ, 1, 8><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
-                                                                  accumulate);
-    else
+                                                                    accumulate);
+    } else {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 1, 4);
       gemm_skinny_nt_kernel<NJ, 1, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
-                                                                  accumulate);
+                                                                    accumulate);
+    }
     return pso_check_launch("pso_gemm(skinny)");
   }
   if (var == 2) {
     const dim3 grid((M + 31) / 32, groups);
+    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 2, 8);
     gemm_skinny_nt_kernel<NJ, 2, 8><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
                                                                 accumulate);
     return pso_check_launch("pso_gemm(skinny)");
   }
   if ((long)((M + 63) / 64) * groups >= 256) {
     const dim3 grid((M + 63) / 64, groups);
+    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 4);
     gemm_skinny_nt_kernel<NJ, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
                                                              accumulate);
   } else {
     const dim3 grid((M + 31) / 32, groups);
+    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 2);
     gemm_skinny_nt_kernel<NJ, 2><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
                                                              accumulate);
   }

@@ -188,10 +188,13 @@ int launch_tnr(int M, int C, const bf16_t* X, long ldx, const bf16_t* U, long ld
   if (spb < 3) spb = 3;
   nmb = (nsteps + spb - 1) / spb;
   const dim3 grid(ncb * nmb);
-  if (out_jc)
+  if (out_jc) {
+    pso_note_kernel("gemm_tn_rank_kernel<%d, true>", NJT);
     gemm_tn_rank_kernel<NJT, true><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
-  else
+  } else {
+    pso_note_kernel("gemm_tn_rank_kernel<%d, false>", NJT);
     gemm_tn_rank_kernel<NJT, false><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
+  }
   return pso_check_launch("pso_gemm_tn(rank)");
 }
 

@@ -28,11 +28,12 @@ def _prof_begin():
 
 
 def _prof_end(e0, flops, nbytes=0.0, tag=None):
-    """nbytes: algorithmic HBM bytes of the launch (every operand read once, the output written once)."""
+    """nbytes: algorithmic HBM bytes of the launch (every operand read once, the output written once).  Each record
+    carries the launched kernel's rocprofv3 name (pso_last_kernel) so timings can be grouped per kernel."""
     if e0 is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        PROFILE.append((flops, nbytes, e0, e1, tag))
+        PROFILE.append((flops, nbytes, e0, e1, tag, lib().pso_last_kernel().decode()))
 
 
 class SideStream:
@@ -98,7 +99,7 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
                          int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
                          ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
                          int(tail_rows), stream_ptr()), "pso_gemm")
-    _prof_end(e0, 2.0 * M * N * (K1 + K2),
+    _prof_end(e0, 2.0 * M * N * K1 + 2.0 * (tail_rows if 0 < tail_rows < M else M) * N * K2,
               2.0 * (M * (K1 + (a2.shape[1] if a2 is not None else 0)) + N * (K1 + K2)) + out.element_size() * M * N,
               ("gemm", M, N, K1, K2, tail_group_n, out.dtype == torch.float32))
     return out

@@ -53,40 +53,50 @@ def main():
         agg[short(n)][0] += 1
         agg[short(n)][1] += d
     tot = sum(v[1] for v in agg.values())
-    fam = [d for _, n, d in trace if any(f in n for f in FAMILY)]
+    dom = rl.get("kernel", "")
     lps = rl.get("launches_per_step")
-    timed = fam[-lps * steps_prof:] if lps else fam
-    fam_avg_us = sum(timed) / max(len(timed), 1) / 1e3
+    mine = [d for _, n, d in trace if short(n).startswith(dom)] if dom else []
+    timed = mine[-lps * steps_prof:] if lps else mine
+    dom_avg_us = sum(timed) / max(len(timed), 1) / 1e3
+    fam = [d for _, n, d in trace if any(f in n for f in FAMILY)]
+    flps = rl.get("family", {}).get("launches_per_step")
+    ftimed = fam[-flps * steps_prof:] if flps else fam
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "
              f"--no-roofline` (C2 config, 1x MI355X)", "",
              f"Whole-run kernel time {tot / 1e9:.3f} s over {len(trace)} dispatches (incl. build + sampling).", "",
              "| kernel | calls | total ms | share | avg us |", "|---|---|---|---|---|"]
     for k, (c, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
         lines.append(f"| `{k}` | {c} | {d / 1e6:.1f} | {100 * d / tot:.2f}% | {d / c / 1e3:.1f} |")
-    lines += ["", "## Dominant kernel family (roofline)", "",
-              f"GEMM family launches in the 2 timed steps: {len(timed)} (bench: {lps} per step)",
-              f"rocprof average launch duration: **{fam_avg_us:.2f} us**; bench.py live HIP-event average: "
-              f"**{rl.get('avg_launch_us')} us** (events add ~1-3 us of record overhead per launch)."]
+    lines += ["", "## Dominant kernel (roofline)", "",
+              f"kernel `{dom}`: {len(timed)} launches in the 2 timed steps (bench: {lps} per step)",
+              f"rocprof average launch duration: **{dom_avg_us:.2f} us**; bench.py live HIP-event average: "
+              f"**{rl.get('avg_launch_us')} us** (an event pair adds ~1-3 us per launch).",
+              f"algorithmic flop per launch {rl.get('flop_per_launch', 0) / 1e9:.2f} GF -> "
+              f"{rl.get('flop_per_launch', 0) / (dom_avg_us * 1e-6) / 1e12 if dom_avg_us else 0:.1f} TF/s on the "
+              f"rocprof duration (bench: {rl.get('achieved')} TF/s)", "",
+              f"GEMM family: {len(ftimed)} launches in the timed steps, rocprof average "
+              f"{sum(ftimed) / max(len(ftimed), 1) / 1e3:.2f} us (bench {rl.get('family', {}).get('achieved')} TF/s)"]
     traffic = None
     pf, pw = load_pmc(os.path.join(root, "pmc_fetch")), load_pmc(os.path.join(root, "pmc_write"))
-    if pf and pw:
+    if pf and pw and dom:
         def last_step(rows):
-            fr = [(i, v) for i, n, c, v in rows if any(f in n for f in FAMILY)]
+            fr = [(i, v) for i, n, c, v in rows if short(n).startswith(dom)]
             return fr[-lps:] if lps else fr
         fs, ws = last_step(pf), last_step(pw)
         # FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
         fetch_b = 2 * 1024 * sum(v for _, v in fs) / max(len(fs), 1)
         write_b = 1024 * sum(v for _, v in ws) / max(len(ws), 1)
         traffic = fetch_b + write_b
-        lines += ["", "## HBM traffic (PMC passes, one train step, GEMM family only)", "",
+        lines += ["", f"## HBM traffic of `{dom}` (PMC passes, one train step)", "",
                   f"launches: fetch pass {len(fs)}, write pass {len(ws)}",
                   f"per launch: FETCH {fetch_b / 1e6:.2f} MB (FETCH_SIZE x 2, gfx950 correction) + WRITE "
                   f"{write_b / 1e6:.2f} MB = **{traffic / 1e6:.2f} MB**"]
         if rl.get("bytes_per_launch"):
-            lines.append(f"algorithmic bytes per launch (A + B + C once): {rl['bytes_per_launch'] / 1e6:.2f} MB")
-        json.dump({"traffic_bytes_per_launch": traffic, "fetch_bytes": fetch_b, "write_bytes": write_b,
-                   "launches": len(fs), "source": f"profiles/{tag}_summary.md"},
-                  open(f"profiles/{tag}_traffic.json", "w"), indent=1)
+            lines.append(f"algorithmic bytes per launch (A + B + C once): {rl['bytes_per_launch'] / 1e6:.2f} MB "
+                         f"(ratio {traffic / rl['bytes_per_launch']:.2f})")
+        json.dump({"kernel": dom, "src_hash": rl.get("src_hash"), "traffic_bytes_per_launch": traffic,
+                   "fetch_bytes": fetch_b, "write_bytes": write_b, "launches": len(fs),
+                   "source": f"profiles/{tag}_summary.md"}, open(f"profiles/{tag}_traffic.json", "w"), indent=1)
     lines += ["", "bench line of the same round:", "", "```", json.dumps(bench), "```"]
     open(f"profiles/{tag}_summary.md", "w").write("\n".join(lines) + "\n")
     stats = glob.glob(os.path.join(root, "prof", "**", "*kernel_stats.csv"), recursive=True)

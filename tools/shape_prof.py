@@ -27,7 +27,7 @@ def main():
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
     agg = defaultdict(lambda: [0, 0.0, 0.0])
-    for fl, nb, e0, e1, tag in rec:
+    for fl, nb, e0, e1, tag, _kname in rec:
         a = agg[tag]
         a[0] += 1
         a[1] += e0.elapsed_time(e1)
