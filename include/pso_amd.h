@@ -175,6 +175,26 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
                        long ld_pre, void* out, long ldo, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
+ * FP8 forward GEMMs (BASELINE config 5: "fp8 MFMA UNet fwd + bf16 bwd").  The reference runs this forward in its
+ * mixed-precision dtype (DB:1815-1825 under accelerate autocast); here the projections fed by a LayerNorm (attention
+ * q/k/v, cross-attention q, the GEGLU ff.net.0.proj) can run on OCP e4m3 operands with one power-of-two scale per
+ * row, stored as an E8M0 byte (127 + exponent; value = e4m3 * 2^exponent).
+ *
+ * pso_quant_rows_fp8: q[m][k] = e4m3(x[m][k] * 2^-e[m]) (round to nearest even, |.| <= 448), e[m] = the smallest
+ *   exponent with rowmax|x| * 2^-e <= 448 (0 for an all-zero row); x bf16 [M][K] (row stride ldx), q [M][K] bytes
+ *   (ldq), e8m0[m] = 127 + e[m].  Used for activations (per token) and weights (per output channel) alike.
+ * pso_gemm_fp8: acc[m][n] = sum_k (a[m][k] 2^ea[m]) (w[n][k] 2^ew[n]) (+ the LoRA K-tail a2 . w2^T on rows < tail_m,
+ *   a2 / w2 fp8 with their own row / column scales, tail_group_n as pso_gemm), fp32 accumulate; epi 0:
+ *   out = bf16(alpha*acc + bias) (+ resid); epi 1: the GEGLU epilogue of pso_gemm_geglu (interleaved weight rows,
+ *   out [M][N/2], out_pre rows < pre_rows).  N % 256 == 0, K % 128 == 0, K2 % 16 == 0, 16-B aligned rows.
+ * ---------------------------------------------------------------------------------------------------------------- */
+int pso_quant_rows_fp8(int M, int K, const void* x, long ldx, void* q, long ldq, void* e8m0, void* stream);
+int pso_gemm_fp8(int epi, int M, int N, int K, const void* a, long lda, const void* sa, const void* w, long ldw,
+                 const void* sw, const void* a2, long lda2, int K2, const void* sa2, const void* w2, long ldw2,
+                 const void* sw2, int tail_m, int tail_group_n, float alpha, const void* bias, const void* resid,
+                 long ldr, void* out, long ldo, void* out_pre, long ld_pre, int pre_rows, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------------
  * DreamBooth PSO loss (config 5), forward and backward to the UNet eps.
  * Replaces: DB = personalization/train_pso_sdxl_turbo_dreambooth.py:1847-1935 -- EDM-style x0 = eps*(-sigma) + noisy,
  *           per-image sigma^-2-weighted MSE vs the clean latent, instance/negative split, pso / pso_db loss, prior

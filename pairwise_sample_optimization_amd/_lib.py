@@ -64,6 +64,9 @@ SIGNATURES = {
     "pso_gemm_skinny_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
     "pso_gemm_geglu": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, vp, cl, vp, cl, ci, vp]),
     "pso_gemm_geglu_bwd": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp]),
+    "pso_quant_rows_fp8": (ci, [ci, ci, vp, cl, vp, cl, vp, vp]),
+    "pso_gemm_fp8": (ci, [ci, ci, ci, ci, vp, cl, vp, vp, cl, vp, vp, cl, ci, vp, vp, cl, vp, ci, ci, cf, vp, vp, cl,
+                          vp, cl, vp, cl, ci, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),
     "pso_group_norm_ws_bytes": (csz, [ci, ci, ci]),

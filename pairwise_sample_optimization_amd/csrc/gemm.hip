@@ -67,8 +67,14 @@ __device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ (r & 7)
 
 template <int BM, int BN, int WAVES>
 struct Tile {
-  static constexpr int A_CH = BM / 8 / WAVES;  // 8-row x 128-B glds pieces per wave per K-tile
-  static constexpr int B_CH = BN / 8 / WAVES;
+  // 8-row x 128-B glds pieces per K-tile (A_P, B_P) and per wave (A_CH, B_CH).  When WAVES does not divide a count
+  // (BN = 160 over 8 waves: 20 pieces), wave w takes pieces w, w + WAVES, ... and the waves left short repeat the last
+  // piece (same source, same bytes, same LDS slot), so every wave issues the same number of loads: counted vmcnt waits
+  // stay uniform.
+  static constexpr int A_P = BM / 8, B_P = BN / 8;
+  static constexpr int A_CH = (A_P + WAVES - 1) / WAVES;
+  static constexpr int B_CH = (B_P + WAVES - 1) / WAVES;
+  static constexpr bool A_EVEN = A_P % WAVES == 0, B_EVEN = B_P % WAVES == 0;
 };
 
 // ---- per-row conv coordinates (precomputed once per thread) ----
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   constexpr int MI = BM / WM / 16;  // 16-row subtiles per wave
   constexpr int NJ = BN / WN / 16;  // 16-col subtiles per wave
   constexpr int PIECES = T::A_CH + T::B_CH;  // glds per wave per K-tile
-  static_assert(T::A_CH * WAVES * 8 == BM && T::B_CH * WAVES * 8 == BN, "tile / wave split");
+  static_assert(BM % 8 == 0 && BN % 8 == 0, "tile / wave split");
   extern __shared__ __attribute__((aligned(16))) bf16_t lds_dyn[];
   bf16_t* lds_base = lds_dyn;
   auto stage_ptr = [&](int s) { return lds_base + s * (BM + BN) * BK; };
@@ -161,6 +167,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  auto pa = [&](int i) { return T::A_EVEN ? wave * T::A_CH + i : min(wave + WAVES * i, T::A_P - 1); };
+  auto pb = [&](int i) { return T::B_EVEN ? wave * T::B_CH + i : min(wave + WAVES * i, T::B_P - 1); };
 
   // XCD-aware block order: blocks b, b+8, b+16 ... share an XCD; give each XCD a contiguous run of tiles.
   const int nbn = (g.N + BN - 1) / BN, nbm = (g.M + BM - 1) / BM;
@@ -211,7 +219,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   RowCoord rc[T::A_CH];
 #pragma unroll
   for (int i = 0; i < T::A_CH; ++i) {
-    const int R = (wave * T::A_CH + i) * 8 + prow;
+    const int R = pa(i) * 8 + prow;
     const int m = min(m0 + R, g.M - 1);
     lcA[i] = pch ^ (R & 7);
     offA[i] = CONV ? 0 : (int)((long)m * g.lda1) + lcA[i] * 8;
@@ -226,7 +234,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   }
 #pragma unroll
   for (int i = 0; i < T::B_CH; ++i) {
-    const int R = (wave * T::B_CH + i) * 8 + prow;
+    const int R = pb(i) * 8 + prow;
     const int n = min(n0 + R, g.N - 1);
     lcB[i] = pch ^ (R & 7);
     offB[i] = (int)((long)n * g.ldb1) + lcB[i] * 8;
@@ -245,7 +253,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
         const TapInfo ti = tap_info(g, k0);
 #pragma unroll
         for (int i = 0; i < T::A_CH; ++i) {
-          const int piece = wave * T::A_CH + i;
+          const int piece = pa(i);
           int iy, ix;
           bool ok;
           if (CONV == PSO_CONV_NORMAL) {
@@ -269,14 +277,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       } else {
 #pragma unroll
         for (int i = 0; i < T::A_CH; ++i) {
-          const int piece = wave * T::A_CH + i;
+          const int piece = pa(i);
           const bool ok = full || k0 + lcA[i] * 8 < K1;
           __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? a1 + offA[i] + k0 : zero), (lds_void*)(la + piece * 8 * BK), 16, 0, 0);
         }
       }
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int piece = wave * T::B_CH + i;
+        const int piece = pb(i);
         const bool ok = full || k0 + lcB[i] * 8 < K1;
         __builtin_amdgcn_global_load_lds(static_cast<const void*>(ok ? b1 + offB[i] + k0 : zero), (lds_void*)(lb + piece * 8 * BK), 16, 0, 0);
       }
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       const int k0 = (t - nt1) * BK;
 #pragma unroll
       for (int i = 0; i < T::A_CH; ++i) {
-        const int piece = wave * T::A_CH + i;
+        const int piece = pa(i);
         const int R = piece * 8 + prow;
         const int mr = m0 + R;
         const int m = min(mr, g.tail_m - 1);
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
       }
 #pragma unroll
       for (int i = 0; i < T::B_CH; ++i) {
-        const int piece = wave * T::B_CH + i;
+        const int piece = pb(i);
         const int R = piece * 8 + prow;
         const int n = min(n0 + R, g.N - 1);
         const int k = k0 + lcB[i] * 8;
@@ -1112,8 +1120,9 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   const hipStream_t st = (hipStream_t)stream;
-  // 8-phase form opt-in (variant 30 / 32): 623 vs 660 TF/s for the 2-phase 128x160 kernel at 8192 x 5120 x 1280
-  if ((g_gemm_variant == 30 || g_gemm_variant == 32) && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) &&
+  // 8-phase form (staggered wave groups) by default: 716 vs 658 TF/s for the 2-phase 128x160 kernel at
+  // 16384 x 5120 x 1280, 489 vs 472 at 65536 x 2560 x 640 (tools/gemm_bench.py, one box); variant 31 keeps 128x160
+  if (g_gemm_variant != 31 && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) &&
       fits30(N, ldw) && (long)((M + 255) / 256) * (N / 256) >= 128)
     return pso_gemm8p_run(2, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, nullptr, nullptr, 0, out,
                           ldo, nullptr, 0, 0, pre, ld_pre, g.group_m, st);

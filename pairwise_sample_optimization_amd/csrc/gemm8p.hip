@@ -24,6 +24,13 @@
 //     steady state.  Phase 4's wait retires the odd K-tile (read in phases 5-8), phase 8's the next even one.
 //   * Each phase: fragment reads, stage, [vmcnt], s_barrier, 16 MFMAs at raised priority, s_barrier.
 // XCD-aware block order and grouped raster as in gemm.hip.
+//
+// FP8 form (the fp8 UNet forward of BASELINE config 5): A / W / A2 / W2 are OCP e4m3 bytes with one power-of-two
+// scale per row of A (and A2) and per output column (row of W, W2), stored as E8M0 bytes (127 + exponent).  A K-tile is
+// 128 deep (the same 128-B rows, so staging and LDS images are byte-for-byte those of the bf16 form); each lane's
+// fragment is 32 consecutive k (two ds_read_b128) and one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 subtile
+// applies the row and column scales in the MFMA (per-lane scale bytes, op_sel picks the subtile's byte), so the
+// accumulator is in true units and the epilogues are the bf16 form's.
 #include "common.h"
 
 #define EPI8_NONE 0
@@ -47,6 +54,8 @@ struct Gemm8Args {
   const bf16_t* aux; long ldaux;        // EPI_GEGLU_BWD: interleaved pre-activation [M][2N]
   int group_m;
   int skip_epi;  // benchmark knob: accumulators kept live, nothing stored (main-loop time alone)
+  // FP8 form: E8M0 scale bytes of the rows of A (M), of W (N), of A2 (tail_m) and of W2 (N)
+  const uint8_t* sa; const uint8_t* sw; const uint8_t* sa2; const uint8_t* sw2;
 };
 
 namespace {
@@ -55,13 +64,30 @@ constexpr int HT = 128 * 64;  // elements of one half-tile image [128 rows][64 k
 
 __device__ __forceinline__ int swz8(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
 
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+template <int V> struct ic8 { static constexpr int value = V; };
+// scaled fp8 MFMA: src0 = W fragment (column scale byte OB of sb), src1 = A fragment (row scale byte OA of sa)
+// As inline asm with the accumulator tied in place: the builtin form needs ~20 more VGPRs at this tile size and
+// spills the accumulators.  op_sel[k] / op_sel_hi[k] = bits 0 / 1 of the scale byte index of scale operand k (0: the
+// src0 = W scale, 1: the src1 = A scale).  Hazards: the scale / fragment registers are written long before (or by LDS
+// reads the compiler waits for), dependent accumulations interlock in hardware, and the epilogue's first VALU read
+// of an accumulator comes after the closing barrier plus an explicit s_nop pad (see the end of the main loop).
+template <int OA, int OB>
+__device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int sa) {
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[%5,%6,0] op_sel_hi:[%7,%8,0]"
+               : "+v"(c)
+               : "v"(w), "v"(x), "v"(sb), "v"(sa), "n"(OB & 1), "n"(OA & 1), "n"(OB >> 1), "n"(OA >> 1));
+}
+
 // STAG: the two wave groups (waves 0-3 / 4-7, one of each per SIMD) run half a phase apart -- waves 4-7 take one
 // extra s_barrier before the main loop, waves 0-3 one after it -- so on every SIMD one wave's MFMA segment runs beside
 // its partner's fragment-read / staging segment (ping-pong).  Every phase then retires its own fragment reads
 // (lgkmcnt(0)) before its first barrier: with the lag, a partner may restage an image one barrier after that point.
 // SPRIO: waves 4-7 hold s_setprio 1 for the whole main loop instead of every wave raising it around its MFMAs.
-template <int EPI, bool STAG, bool SPRIO>
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
+  constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
+  constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
   extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1][HT]
   const int tid = threadIdx.x, lane = tid & 63;
   // wave index in an SGPR: the LDS-DMA destinations (M0) are then scalar arithmetic, not 8 spilled VGPR addresses
@@ -87,9 +113,9 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     bn = in / gsz;
   }
   const int m0 = bm * 256, n0 = bn * 256;
-  const int nt1 = g.K / 64;  // K % 64 == 0 (host-checked)
+  const int nt1 = g.K / KT;  // K % KT == 0 (host-checked)
   // the LoRA K-tail: tiles made only of rows >= tail_m (the reference half of a paired pass) skip it (zero there)
-  const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + 63) / 64 : 0;
+  const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + KT - 1) / KT : 0;
   const int nt = (nt1 + nt2 + 1) & ~1;  // the 8-phase loop consumes K-tiles in pairs: an odd count gets a zero tile
 
   // staging: wave w fills pieces 2w, 2w+1 (8 rows x 128 B each) of every half-tile image; the XOR swizzle is applied
@@ -105,8 +131,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     for (int i = 0; i < 2; ++i) {
       const int R = (wave * 2 + i) * 8 + prow;
       const int lc = pch ^ (R & 7);
-      aoff[h][i] = (unsigned)(min(m0 + h * 128 + R, g.M - 1) * (int)g.lda + lc * 8) * 2u;
-      woff[h][i] = (unsigned)((n0 + h * 128 + R) * (int)g.ldw + lc * 8) * 2u;
+      aoff[h][i] = (unsigned)(min(m0 + h * 128 + R, g.M - 1) * (int)g.lda * ES + lc * 16);
+      woff[h][i] = (unsigned)((n0 + h * 128 + R) * (int)g.ldw * ES + lc * 16);
     }
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
@@ -132,7 +158,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
                                                  0);
       }
     } else {  // LoRA K-tail (one or two K-tiles per output tile) or the zero pad tile
-      const int kc = (kt - nt1) * 64 + (pch ^ prow) * 8;  // this lane's 8 columns of the tail
+      const int kc = (kt - nt1) * KT + (pch ^ prow) * (16 / ES);  // this lane's 16-B chunk of the tail
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -140,10 +166,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
         unsigned off;
         if (half < 2) {
           const int m = m0 + R;
-          off = (kin && m < g.tail_m) ? (unsigned)(((long)m * g.lda2 + a2_col + kc) * 2) : OOB;
+          off = (kin && m < g.tail_m) ? (unsigned)(((long)m * g.lda2 + a2_col + kc) * ES) : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rA2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
         } else {
-          off = kin ? (unsigned)(((long)(n0 + R) * g.ldw2 + kc) * 2) : OOB;
+          off = kin ? (unsigned)(((long)(n0 + R) * g.ldw2 + kc) * ES) : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rW2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
         }
       }
@@ -160,18 +186,24 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 af[2][2], bfr[4][2];  // [row subtile][kk], [col subtile][kk]
+  bf16x8 af[2][2], bfr[4][2];  // [row subtile][kk], [col subtile][kk]  (bf16 form)
+  i32x8 af8[2], bf8[4];         // FP8 form: [row subtile], [col subtile], 32 fp8 k per lane (two 16-B reads)
   // Fragment addresses: the swizzle term depends only on fr & 7, so within an image a lane needs one byte offset per
   // kk (subtiles are +2048-B immediates).  The image base is added per read by a volatile v_add: left to itself the
   // compiler hoists 8 images x 4 addresses out of the loop and spills at this register budget.
   typedef __attribute__((address_space(3))) const bf16x8 lds_frag;
+  typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+  typedef __attribute__((address_space(3))) const i32x4_t lds_frag4;
   const unsigned l8base = (unsigned)(uintptr_t)(lds8_void*)l8;
   unsigned la[2], lb[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    la[kk] = (unsigned)swz8(wr * 32 + fr, kk * 4 + fk) * 2u;
-    lb[kk] = (unsigned)swz8(wc * 64 + fr, kk * 4 + fk) * 2u;
+    // bf16: 8-element chunk kk*4 + fk (k = 32 kk + 8 fk ..); fp8: the lane's 32 consecutive k are chunks 2 fk, 2 fk + 1
+    const int ch = FP8 ? 2 * fk + kk : kk * 4 + fk;
+    la[kk] = (unsigned)swz8(wr * 32 + fr, ch) * 2u;
+    lb[kk] = (unsigned)swz8(wc * 64 + fr, ch) * 2u;
   }
+  i32x4_t ta[2], tb[4];
   auto read_a = [&](int img) {
     const unsigned ib = l8base + (unsigned)(img * HT * 2);
 #pragma unroll
@@ -179,7 +211,14 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       unsigned ad;
       asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(la[kk]));
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i][kk] = *(lds_frag*)(uintptr_t)(ad + i * 2048);
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (FP8) {
+          if (kk == 0) ta[i] = *(lds_frag4*)(uintptr_t)(ad + i * 2048);
+          else af8[i] = __builtin_shufflevector(ta[i], *(lds_frag4*)(uintptr_t)(ad + i * 2048), 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+          af[i][kk] = *(lds_frag*)(uintptr_t)(ad + i * 2048);
+        }
+      }
     }
   };
   auto read_b = [&](int img) {
@@ -189,18 +228,75 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       unsigned ad;
       asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb[kk]));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j][kk] = *(lds_frag*)(uintptr_t)(ad + j * 2048);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (FP8) {
+          if (kk == 0) tb[j] = *(lds_frag4*)(uintptr_t)(ad + j * 2048);
+          else bf8[j] = __builtin_shufflevector(tb[j], *(lds_frag4*)(uintptr_t)(ad + j * 2048), 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+          bfr[j][kk] = *(lds_frag*)(uintptr_t)(ad + j * 2048);
+        }
+      }
     }
   };
-  auto mfma_q = [&](int ha, int hb) {
+  // FP8: scale bytes of this lane's rows (byte 2 ha + i) and columns (byte j of word hb), main and tail operands
+  int sra = 0, srb[2] = {0, 0}, sra2 = 0, srb2[2] = {0, 0};
+  if constexpr (FP8) {
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = m0 + ha * 128 + wr * 32 + i * 16 + fr;
+        sra |= (int)g.sa[min(m, g.M - 1)] << (8 * (2 * ha + i));
+        if (g.a2) sra2 |= (int)g.sa2[min(m, g.tail_m - 1)] << (8 * (2 * ha + i));
+      }
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + hb * 128 + wc * 64 + j * 16 + fr;
+        srb[hb] |= (int)g.sw[n] << (8 * j);
+        if (g.a2) srb2[hb] |= (int)g.sw2[n] << (8 * j);
+      }
+  }
+  auto mfma_q = [&](auto HA_, auto HB_, bool tail_start) {
+    constexpr int ha = decltype(HA_)::value, hb = decltype(HB_)::value;
+    if constexpr (FP8) {
+      // first quadrant of the first LoRA K-tail tile: from here on the tail operands' scales (in asm, with the wait
+      // states an MFMA scale operand needs after a VALU write -- the asm MFMAs are invisible to the hazard recognizer)
+      if (ha == 0 && hb == 0 && tail_start)
+        asm volatile("v_mov_b32 %0, %3\n\tv_mov_b32 %1, %4\n\tv_mov_b32 %2, %5\n\ts_nop 7"
+                     : "=v"(sra), "=v"(srb[0]), "=v"(srb[1])
+                     : "v"(sra2), "v"(srb2[0]), "v"(srb2[1]));
+    }
     if (!SPRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (FP8) {
+      auto q8 = [&](int sa, int sb) {
+        mfma8s<2 * ha, 0>(bf8[0], af8[0], acc[ha][hb][0][0], sb, sa);
+        mfma8s<2 * ha, 1>(bf8[1], af8[0], acc[ha][hb][0][1], sb, sa);
+        mfma8s<2 * ha, 2>(bf8[2], af8[0], acc[ha][hb][0][2], sb, sa);
+        mfma8s<2 * ha, 3>(bf8[3], af8[0], acc[ha][hb][0][3], sb, sa);
+        mfma8s<2 * ha + 1, 0>(bf8[0], af8[1], acc[ha][hb][1][0], sb, sa);
+        mfma8s<2 * ha + 1, 1>(bf8[1], af8[1], acc[ha][hb][1][1], sb, sa);
+        mfma8s<2 * ha + 1, 2>(bf8[2], af8[1], acc[ha][hb][1][2], sb, sa);
+        mfma8s<2 * ha + 1, 3>(bf8[3], af8[1], acc[ha][hb][1][3], sb, sa);
+      };
+      q8(sra, srb[hb]);
+      // The hazard recognizer cannot see into the asm: a register copy of an accumulator placed right behind it (the
+      // allocator's loop-carried copies) would read the MFMA's destination before it is written.  Route the
+      // quadrant's accumulators through one more asm holding the VALU-read wait states, so every later use follows it.
+      asm volatile("s_nop 11"
+                   : "+v"(acc[ha][hb][0][0]), "+v"(acc[ha][hb][0][1]), "+v"(acc[ha][hb][0][2]), "+v"(acc[ha][hb][0][3]),
+                     "+v"(acc[ha][hb][1][0]), "+v"(acc[ha][hb][1][1]), "+v"(acc[ha][hb][1][2]), "+v"(acc[ha][hb][1][3]));
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[ha][hb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j)
+            acc[ha][hb][i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
+    }
     if (!SPRIO) __builtin_amdgcn_s_setprio(0);
   };
   // one phase: reads (RA / RB: which operand image to (re)load), the stage (if its K-tile exists), the optional
@@ -215,7 +311,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     else if ((VM) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                      \
     __builtin_amdgcn_s_barrier();                                                             \
     __builtin_amdgcn_sched_barrier(0);                                                        \
-    mfma_q((HA), (HB));                                                                       \
+    mfma_q(ic8<(HA)>{}, ic8<(HB)>{}, FP8 && nt2 > 0 && j + (BUF) == nt1);                     \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     __builtin_amdgcn_s_barrier();                                                             \
   }
@@ -245,6 +341,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     else { PHASE(1, 0, 1, 1, 0, j + 3, 7, -1) }
   }
 #undef PHASE
+  // FP8: the inline-asm MFMAs are invisible to the hazard recognizer -- pad before any VALU reads an accumulator
+  if constexpr (FP8) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   if (STAG && wave < 4) __builtin_amdgcn_s_barrier();
   if (SPRIO) __builtin_amdgcn_s_setprio(0);
 
@@ -377,19 +475,20 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   }
 }
 
-template <int EPI, bool STAG, bool SPRIO>
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false>
 int launch8(const Gemm8Args& g, hipStream_t st) {
   const int nblk = ((g.M + 255) / 256) * (g.N / 256);
   const size_t shm = 8 * HT * sizeof(bf16_t);  // 128 KiB
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)shm);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
-  pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
-  gemm8p_kernel<EPI, STAG, SPRIO><<<nblk, 512, shm, st>>>(g);
-  return pso_check_launch("pso_gemm(8-phase)");
+  if (FP8) pso_note_kernel("gemm8p_kernel<%d, true, false, true>", EPI);
+  else pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
+  gemm8p_kernel<EPI, STAG, SPRIO, FP8><<<nblk, 512, shm, st>>>(g);
+  return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
 }
 
 template <int EPI>
@@ -428,4 +527,39 @@ int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const 
   if (epi == EPI8_GEGLU) return launch8s<EPI8_GEGLU>(g, st, g_mode8);
   if (epi == EPI8_GEGLU_BWD) return launch8s<EPI8_GEGLU_BWD>(g, st, g_mode8);
   return launch8s<EPI8_NONE>(g, st, g_mode8);
+}
+
+// FP8 form (pso_amd.h, pso_gemm_fp8): staggered wave groups, epilogue 0 (bias / alpha / residual) or 1 (GEGLU)
+extern "C" int pso_gemm_fp8(int epi, int M, int N, int K, const void* a, long lda, const void* sa, const void* w,
+                            long ldw, const void* sw, const void* a2, long lda2, int K2, const void* sa2,
+                            const void* w2, long ldw2, const void* sw2, int tail_m, int tail_group_n, float alpha,
+                            const void* bias, const void* resid, long ldr, void* out, long ldo, void* out_pre,
+                            long ld_pre, int pre_rows, void* stream) {
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  PSO_ARG_CHECK(epi == EPI8_NONE || epi == EPI8_GEGLU, "pso_gemm_fp8: epi must be 0 (plain) or 1 (GEGLU)");
+  PSO_ARG_CHECK(M > 0 && N > 0 && (N % 256) == 0 && K > 0 && (K % 128) == 0,
+                "pso_gemm_fp8: need N %% 256 == 0, K %% 128 == 0 (M=%d N=%d K=%d)", M, N, K);
+  PSO_ARG_CHECK(a && sa && w && sw && out, "pso_gemm_fp8: null operand");
+  PSO_ARG_CHECK(a16(a) && a16(w) && (lda % 16) == 0 && (ldw % 16) == 0 && a16(out) && (ldo % 8) == 0,
+                "pso_gemm_fp8: A / W / out need 16-B aligned rows");
+  PSO_ARG_CHECK((long)M * lda < (1L << 31) && (long)N * ldw < (1L << 31), "pso_gemm_fp8: operand above 2 GiB");
+  PSO_ARG_CHECK(!a2 || (w2 && sa2 && sw2 && K2 > 0 && (K2 % 16) == 0 && a16(a2) && a16(w2) && (lda2 % 16) == 0 &&
+                        (ldw2 % 16) == 0 && tail_m > 0 && (long)tail_m * lda2 < (1L << 31) &&
+                        (tail_group_n == 0 || (tail_group_n % 256) == 0)),
+                "pso_gemm_fp8: bad LoRA tail operands");
+  PSO_ARG_CHECK(!resid || (a16(resid) && (ldr % 8) == 0), "pso_gemm_fp8: residual needs 16-B aligned rows");
+  PSO_ARG_CHECK(epi != EPI8_GEGLU || (bias && !resid && (!out_pre || (a16(out_pre) && (ld_pre % 8) == 0))),
+                "pso_gemm_fp8: GEGLU needs a bias, no residual, aligned out_pre");
+  Gemm8Args g{};
+  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
+  g.M = M; g.N = N; g.K = K;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0; g.w2 = (const bf16_t*)w2; g.ldw2 = ldw2;
+  g.tail_m = a2 ? (tail_m < M ? tail_m : M) : M; g.tail_group_n = a2 ? tail_group_n : 0;
+  g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out2 = out_pre; g.ldo2 = ld_pre; g.pre_rows = pre_rows > 0 ? pre_rows : M;
+  g.group_m = 4; g.skip_epi = g_skip_epi8;
+  g.sa = (const uint8_t*)sa; g.sw = (const uint8_t*)sw; g.sa2 = (const uint8_t*)sa2; g.sw2 = (const uint8_t*)sw2;
+  const hipStream_t st = (hipStream_t)stream;
+  if (epi == EPI8_GEGLU) return launch8<EPI8_GEGLU, true, false, true>(g, st);
+  return launch8<EPI8_NONE, true, false, true>(g, st);
 }

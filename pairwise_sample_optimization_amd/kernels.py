@@ -178,6 +178,57 @@ def gemm_geglu_bwd(a, w, pre, out=None):
     return out
 
 
+def quant_rows_fp8(x, q=None, e=None):
+    """Row-wise OCP e4m3 quantisation with a power-of-two scale per row: returns (q uint8 [M, K], e uint8 [M]) with
+    x[m] ~= e4m3(q[m]) * 2^(e[m] - 127) (pso_quant_rows_fp8; activations per token, weights per output channel)."""
+    require_cuda(x)
+    assert x.dtype == BF16 and x.dim() == 2
+    M, Kd = x.shape
+    if q is None:
+        q = torch.empty((M, Kd), device=x.device, dtype=torch.uint8)
+    if e is None:
+        e = torch.empty((M,), device=x.device, dtype=torch.uint8)
+    check(lib().pso_quant_rows_fp8(M, Kd, ptr(x), _row_stride(x), ptr(q), _row_stride(q), ptr(e), stream_ptr()),
+          "pso_quant_rows_fp8")
+    return q, e
+
+
+def dequant_rows_fp8(q, e):
+    """Host-side view of quant_rows_fp8's output as fp32 (tests / references only)."""
+    return q.view(torch.float8_e4m3fn).float() * torch.exp2(e.float() - 127.0)[:, None]
+
+
+def gemm_fp8(a, w, *, a2=None, w2=None, tail_rows=0, tail_group_n=0, alpha=1.0, bias=None, resid=None, out=None,
+             geglu=False, out_pre=None, pre_rows=0):
+    """fp8 forward GEMM (pso_gemm_fp8): a = (q [M, K], e [M]) and w = (q [N, K], e [N]) from quant_rows_fp8, likewise
+    the LoRA tail a2 [tail_rows or M, K2*groups] / w2 [N, K2].  Plain: out [M, N] = bf16(alpha*acc + bias) (+ resid);
+    geglu: the GEGLU epilogue of gemm_geglu on interleaved weight rows (out [M, N/2], out_pre rows < pre_rows)."""
+    (aq, ae), (wq, we) = a, w
+    require_cuda(aq, wq)
+    M, Kd = aq.shape
+    N = wq.shape[0]
+    assert wq.shape[1] == Kd and aq.dtype == torch.uint8 and wq.dtype == torch.uint8
+    K2, tr = 0, (tail_rows if 0 < tail_rows < M else M)
+    if a2 is not None:
+        K2 = w2[0].shape[1]
+        assert a2[0].shape[0] == tr and w2[0].shape[0] == N
+    if out is None:
+        out = torch.empty((M, N // 2 if geglu else N), device=aq.device, dtype=BF16)
+    e0 = _prof_begin()
+    check(lib().pso_gemm_fp8(1 if geglu else 0, M, N, Kd, ptr(aq), _row_stride(aq), ptr(ae), ptr(wq), _row_stride(wq),
+                             ptr(we), ptr(a2[0]) if a2 is not None else None,
+                             _row_stride(a2[0]) if a2 is not None else 0, K2,
+                             ptr(a2[1]) if a2 is not None else None, ptr(w2[0]) if a2 is not None else None,
+                             _row_stride(w2[0]) if a2 is not None else 0, ptr(w2[1]) if a2 is not None else None,
+                             tr, int(tail_group_n), float(alpha), ptr(bias), ptr(resid),
+                             _row_stride(resid) if resid is not None else 0, ptr(out), _row_stride(out),
+                             ptr(out_pre), _row_stride(out_pre) if out_pre is not None else 0, int(pre_rows),
+                             stream_ptr()), "pso_gemm_fp8")
+    _prof_end(e0, 2.0 * M * N * Kd + 2.0 * tr * N * K2, 1.0 * (M * Kd + N * Kd) + 2.0 * M * N,
+              ("gemm_fp8", M, N, Kd, K2, tail_group_n, geglu))
+    return out
+
+
 TN_RANKS = (32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
 
 

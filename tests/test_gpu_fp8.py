@@ -1,0 +1,103 @@
+"""GPU parity of the fp8 forward path (BASELINE config 5: fp8 MFMA UNet forward): row-wise e4m3 quantisation against
+torch's float8_e4m3fn cast, and the scaled-MFMA GEMM (pso_gemm_fp8) against a torch fp32 product of the SAME dequantised
+operands (so the bar measures the kernel, not the quantisation), plus its distance to the unquantised bf16 product."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _rows(M, K, cuda, g, spread=12):
+    """bf16 rows whose magnitudes span 2^-spread .. 2^spread (exercises the per-row exponents)."""
+    x = torch.randn(M, K, device=cuda, generator=g)
+    s = torch.exp2(torch.randint(-spread, spread + 1, (M, 1), device=cuda, generator=g).float())
+    return (x * s).bfloat16()
+
+
+@pytest.mark.parametrize("M,K", [(300, 1280), (4096, 640), (7, 5120), (64, 8)])
+def test_quant_rows_fp8_matches_torch_cast(cuda, M, K):
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    x = _rows(M, K, cuda, g)
+    x[0] = 0  # all-zero row: exponent 0, all-zero codes
+    q, e = K_.quant_rows_fp8(x)
+    amax = x.float().abs().amax(1)
+    ex = torch.where(amax > 0, torch.ceil(torch.log2(amax / 448.0)), torch.zeros_like(amax))
+    assert torch.equal(e.long() - 127, ex.long())
+    ref = (x.float() * torch.exp2(-ex)[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(q, ref)
+    deq = K_.dequant_rows_fp8(q, e)
+    assert q.view(torch.float8_e4m3fn).float().abs().amax() <= 448.0  # scaled rows stay in e4m3 range
+    assert _rel(deq, x) < 4e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1280, 1280), (1000, 768, 640), (300, 256, 128), (2048, 3840, 1280),
+                                   (257, 512, 384)])
+def test_gemm_fp8_vs_fp32_on_dequantised_operands(cuda, M, N, K):
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
+    x = _rows(M, K, cuda, g)
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda, generator=g).bfloat16()
+    r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    xa, wa = K_.quant_rows_fp8(x), K_.quant_rows_fp8(w)
+    ref_acc = K_.dequant_rows_fp8(*xa) @ K_.dequant_rows_fp8(*wa).t()
+    sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+    out = sentinel[:M]
+    K_.gemm_fp8(xa, wa, alpha=0.75, bias=b, resid=r, out=out)
+    ref = (0.75 * ref_acc + b.float()).bfloat16().float() + r.float()
+    assert _rel(out, ref) < 4e-3
+    assert (sentinel[M:] == 7.0).all()
+    # the quantisation error itself, against the unquantised bf16 operands
+    full = 0.75 * (x.float() @ w.float().t()) + b.float() + r.float()
+    assert _rel(out, full) < 6e-2
+
+
+@pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(4096, 3840, 1280, 32, 1280, 2048), (1000, 768, 640, 32, 256, 0),
+                                                      (2048, 1280, 1280, 32, 0, 1024), (520, 512, 256, 48, 512, 300)])
+def test_gemm_fp8_lora_tail(cuda, M, N, K, K2, group, tail_rows):
+    """LoRA up-projection as an fp8 K-tail with its own row / column scales, grouped per output block (fused q/k/v) and
+    limited to the policy rows of a paired pass."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + K2)
+    x = _rows(M, K, cuda, g, spread=4)
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    tr = tail_rows or M
+    ng = N // group if group else 1
+    u = _rows(tr, K2 * ng, cuda, g, spread=6)
+    w2 = (torch.randn(N, K2, device=cuda, generator=g) / 60).bfloat16()
+    xa, wa, ua, w2a = (K_.quant_rows_fp8(t) for t in (x, w, u, w2))
+    y = K_.dequant_rows_fp8(*xa) @ K_.dequant_rows_fp8(*wa).t()
+    ud, w2d = K_.dequant_rows_fp8(*ua), K_.dequant_rows_fp8(*w2a)
+    for j in range(ng):
+        cs = slice(j * group, (j + 1) * group) if group else slice(0, N)
+        y[:tr, cs] += ud[:, K2 * j:K2 * (j + 1)] @ w2d[cs].t()
+    out = K_.gemm_fp8(xa, wa, a2=ua, w2=w2a, tail_rows=tail_rows, tail_group_n=group)
+    assert _rel(out, y) < 4e-3
+    if tr < M:
+        assert _rel(out[tr:], y[tr:]) < 4e-3
+
+
+@pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0)])
+def test_gemm_fp8_geglu(cuda, M, Fd, K, pre_rows):
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M + Fd)
+    x = _rows(M, K, cuda, g, spread=3)
+    wp = (torch.randn(2 * Fd, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    bp = torch.randn(2 * Fd, device=cuda, generator=g).bfloat16()
+    idx = K_.geglu_interleave_index(Fd, cuda)
+    xa, wa = K_.quant_rows_fp8(x), K_.quant_rows_fp8(wp[idx].contiguous())
+    pr = pre_rows or M
+    pre = torch.empty(pr, 2 * Fd, device=cuda, dtype=torch.bfloat16)
+    out = K_.gemm_fp8(xa, wa, bias=bp[idx].contiguous(), geglu=True, out_pre=pre, pre_rows=pre_rows)
+    inv = torch.argsort(idx)
+    wd = K_.dequant_rows_fp8(*wa)[inv]  # back to diffusers [h rows; gate rows]
+    hg = (K_.dequant_rows_fp8(*xa) @ wd.t() + bp.float()).bfloat16().float()
+    h, gt = hg[:, :Fd], hg[:, Fd:]
+    assert _rel(out, h * F.gelu(gt)) < 4e-3
+    assert _rel(pre, hg[:pr, idx]) < 4e-3
