@@ -332,6 +332,7 @@ class LoraState:
 
     def refresh(self):
         """bf16 working copies (B pre-scaled by alpha/r) and their transposed forms after a master update."""
+        self.version = getattr(self, "version", 0) + 1  # keys the fp8 copies of the sB stacks (fp8 forward)
         K.cast_f32_bf16(self.master, out=self.work)
         if self.scale != 1.0:
             for Bw in self._b_views:
@@ -422,9 +423,21 @@ class BasicTransformerBlock(nn.Module):
         pol = (lambda t: t[:t.shape[0] // 2]) if rt.paired else (lambda t: t)
         # --- self attention: fused q/k/v projection, the three LoRA up-projections as a grouped K-tail ---
         n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
+        f8 = rt.fp8  # fp8 forward (config 5): the LayerNorm-fed projections on e4m3 MFMA where the shapes allow
+        # (the fp8 LoRA tail reads 16-B rows of the rank-r operands: r % 16 == 0)
+        ok8 = lambda n_out, k_in: (f8 is not None and n_out % 256 == 0 and k_in % 128 == 0 and
+                                   (not lo or rt.r % 16 == 0))
+        ver = rt.lora.version if lo else 0
         if lo:
             u_qkv = K.gemm(pol(n1), L.A_qkv)                                # [Mp, 3r]
-            qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
+            if ok8(3 * C, C):
+                qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv),
+                                 a2=K.quant_rows_fp8(u_qkv), w2=f8((id(self), "sB_qkv"), L.sB_qkv, ver),
+                                 tail_group_n=C, tail_rows=tr)
+            else:
+                qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
+        elif ok8(3 * C, C):
+            qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv))
         else:
             qkv = K.gemm(n1, a1m.w_qkv)
         q3 = qkv.view(B, S, 3 * C)
@@ -442,7 +455,13 @@ class BasicTransformerBlock(nn.Module):
         Se = enc.shape[0] // B
         if lo:
             u_q2 = K.gemm(pol(n2), L.A_q2)
-            q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
+            if ok8(C, C):
+                q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight),
+                                a2=K.quant_rows_fp8(u_q2), w2=f8((id(self), "sB_q2"), L.sB_q2, ver), tail_rows=tr)
+            else:
+                q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
+        elif ok8(C, C):
+            q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight))
         else:
             q2 = K.gemm(n2, a2m.to_q.weight)
         # K/V of the text tokens: this block's columns of the width-batched projection (UNet2DConditionModel.kv_text)
@@ -462,7 +481,11 @@ class BasicTransformerBlock(nn.Module):
         n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
         ff = self.ff
         f = torch.empty((Mp, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
-        gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f, pre_rows=Mp)  # f: interleaved pre-activation (bwd)
+        if ok8(ff.w_int.shape[0], C):
+            gg = K.gemm_fp8(K.quant_rows_fp8(n3), f8((id(self), "ff"), ff.w_int), bias=ff.b_int, geglu=True, out_pre=f,
+                            pre_rows=Mp)
+        else:
+            gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f, pre_rows=Mp)  # f: interleaved pre-activation (bwd)
         h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
         if rt.save:  # the backward runs on the policy images only
             sv = dict(x=pol(x), st1=pol(st1), n1=pol(n1), qkv=pol(qkv), a1=pol(a1), lse1=pol(lse1), h1=pol(h1),
@@ -858,6 +881,8 @@ class UNet2DConditionModel(nn.Module):
         self.conv_out = Conv2d(ch[0], cfg.out_channels, 3)
         self.lora = None
         self.full = None  # FullGradState when every parameter is trained (C3 / C4)
+        self.fp8 = False  # fp8 forward of the LayerNorm-fed projections (enable_fp8_forward, config 5)
+        self._fp8_cache = {}
         self._adapters_enabled = True
         self._prepared = False
         self.gradient_checkpointing = False
@@ -1052,11 +1077,34 @@ class UNet2DConditionModel(nn.Module):
                         self.add_embedding.linear_2):
                 lin.prepare()
         self._prepared = True
+        self._fp8_cache = {}  # kernel-layout weights may have been rebuilt
         if self.lora is not None:
             self.refresh_lora()
 
     def refresh_lora(self):
         self.lora.refresh()
+
+    # ---------------- fp8 forward (BASELINE config 5) ----------------
+    def enable_fp8_forward(self, on=True):
+        """Run the LayerNorm-fed projections of every transformer block -- the fused self-attention q/k/v, the
+        cross-attention q and the GEGLU ff.net.0.proj, 2/3 of a block's projection FLOPs -- on fp8 e4m3 MFMA
+        (pso_gemm_fp8: per-token activation scales, per-output-channel weight scales, the LoRA up-projection as an fp8
+        K-tail); everything else, and the whole backward, stays bf16 (BASELINE config 5: "fp8 MFMA UNet fwd + bf16
+        bwd").  Shapes the fp8 kernel does not take (N % 256 or K % 128 != 0: the 640-wide q/k/v of the 64^2 level)
+        stay bf16.  LoRA training only (the base weights are quantised once and cached)."""
+        if on and self.full is not None:
+            raise ValueError("fp8 forward: LoRA training only (the full-UNet mode updates the base weights)")
+        self.fp8 = bool(on)
+        self._fp8_cache = {}
+        return self
+
+    def _fp8_weight(self, key, w, version=0):
+        """(e4m3 [N, K], E8M0 [N]) of a weight, quantised per output channel once per (key, version)."""
+        hit = self._fp8_cache.get(key)
+        if hit is None or hit[0] != version:
+            hit = (version, K.quant_rows_fp8(w))
+            self._fp8_cache[key] = hit
+        return hit[1]
 
     def kv_text(self, rt, C):
         """K/V of the text tokens for every block of width C: ([rows, n*2C], LoRA down-projection [policy rows, n*2r]
@@ -1086,6 +1134,7 @@ class UNet2DConditionModel(nn.Module):
         rt.kv_text = lambda C: self.kv_text(rt, C)
         rt.lora = self.lora
         rt.r = self.lora.r if lora_on else 0
+        rt.fp8 = self._fp8_weight if self.fp8 else None
         return rt
 
     def _embed(self, timestep, time_ids, text_embeds, B, dev):

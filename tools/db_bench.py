@@ -1,6 +1,7 @@
 """DreamBooth PSO micro-step throughput (BASELINE config 5 shape on one GPU: SDXL-Turbo UNet + SDXL VAE encoder,
-LoRA r=16, B=1 instance + 1 negative per micro-step, bf16; the fp8 forward of config 5 is not built -- DESIGN.md).
-Prints one JSON line.  usage: python tools/db_bench.py [--res 1024] [--steps 5] [--warmup 2] [--loss pso_db|pso]"""
+LoRA r=16, B=1 instance + 1 negative per micro-step; bf16, or --fp8: the config-5 fp8 forward of the LayerNorm-fed
+projections with the bf16 backward).  Prints one JSON line.
+usage: python tools/db_bench.py [--res 1024] [--steps 5] [--warmup 2] [--loss pso_db|pso] [--batch B] [--fp8]"""
 import argparse
 import json
 import os
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--rank", type=int, default=16)
     ap.add_argument("--loss", default="pso_db")
+    ap.add_argument("--fp8", action="store_true")
     a = ap.parse_args()
     from pairwise_sample_optimization_amd.dreambooth import DreamBoothPSOTrainer
     from pairwise_sample_optimization_amd.trainer import compute_time_ids
@@ -37,6 +39,8 @@ def main():
     unet.add_adapter(SimpleNamespace(r=a.rank, lora_alpha=a.rank))
     unet.lora.init_gaussian(seed=0, b_std=1e-3)
     unet.prepare()
+    if a.fp8:
+        unet.enable_fp8_forward()
     tr = DreamBoothPSOTrainer(unet, vae, loss_type=a.loss, beta_pso=5.0 if a.loss == "pso_db" else 200.0,
                               gradient_accumulation_steps=4)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -55,8 +59,10 @@ def main():
     dt = (time.perf_counter() - t0) / a.steps
     print(json.dumps({"metric": "DreamBooth PSO micro-step imgs/sec (instance + negative, SDXL-Turbo)",
                       "value": round(2 * B / dt, 3), "unit": "imgs/s", "ms_per_step": round(dt * 1e3, 2),
-                      "n_gpus": 1, "steps": a.steps, "dtype": "bf16", "data": "synthetic",
-                      "config": {"workload": f"C5 (1 GPU, bf16 fwd): DreamBooth PSO {a.loss}, LoRA r={a.rank}, "
+                      "n_gpus": 1, "steps": a.steps,
+                      "dtype": "fp8 e4m3 fwd (LayerNorm-fed projections) + bf16" if a.fp8 else "bf16",
+                      "data": "synthetic",
+                      "config": {"workload": f"C5 (1 GPU, {'fp8' if a.fp8 else 'bf16'} fwd): DreamBooth PSO {a.loss}, LoRA r={a.rank}, "
                                              f"{B} instance + {B} negative, gas 4, VAE encode in the step",
                                  "resolution": a.res},
                       "loss": round(torch.stack(tr.loss_hist[-2:]).mean().item(), 6)}))
