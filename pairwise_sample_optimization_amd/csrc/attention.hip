@@ -670,7 +670,8 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         }
 #pragma unroll
         for (int kj = 0; kj < KJ; ++kj) {
-          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+          // dP accumulates onto -delta (register r = query 4g + r), so dS = P * acc: one VALU op per score less
+          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {-dq_[0], -dq_[1], -dq_[2], -dq_[3]};
           sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[0], kf[kj][0], sacc, 0, 0, 0);
           sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[1], kf[kj][1], sacc, 0, 0, 0);
           pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[0], vf[kj][0], pacc, 0, 0, 0);
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
           for (int r = 0; r < 4; ++r) {
             const float pr = fast_exp2(fmaf(sacc[r], c2, -lq[r]));
             p[qh][kj][r] = pr;
-            dsv[qh][kj][r] = pr * (pacc[r] - dq_[r]);
+            dsv[qh][kj][r] = pr * pacc[r];
           }
         }
       }
@@ -817,6 +818,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     const bf16_t* sKt = sRing[kt % STG][1];
     const bf16_t* sVr = sRing[kt % STG][2];
     const int kbase = kt * ATT_KT;
+    const bool kpart = kbase + ATT_KT > a.Sk;  // wave-uniform
     f32x4 dsT[2][4];  // lane holds dS[q = qi*16 + c][key = kj*16 + 4g + r]
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {
@@ -828,16 +830,22 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
       }
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi) {
-        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+        // dP^T accumulates onto -delta of this lane's query (one VALU op per score less)
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {-dl[qi], -dl[qi], -dl[qi], -dl[qi]};
         sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[0], qf[qi][0], sacc, 0, 0, 0);
         sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qi][1], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], of[qi][0], pacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[1], of[qi][1], pacc, 0, 0, 0);
+        if (kpart) {  // last, partial key tile only: padded keys get p = 0
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kbase + kj * 16 + 4 * g + r;
-          const float p = key < a.Sk ? fast_exp2(sacc[r] * a.scale_log2 - lq[qi]) : 0.f;
-          dsT[qi][kj][r] = p * (pacc[r] - dl[qi]);
+          for (int r = 0; r < 4; ++r) {
+            const int key = kbase + kj * 16 + 4 * g + r;
+            const float p = key < a.Sk ? fast_exp2(fmaf(sacc[r], a.scale_log2, -lq[qi])) : 0.f;
+            dsT[qi][kj][r] = p * pacc[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dsT[qi][kj][r] = fast_exp2(fmaf(sacc[r], a.scale_log2, -lq[qi])) * pacc[r];
         }
       }
     }
