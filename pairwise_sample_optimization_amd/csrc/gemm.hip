@@ -766,6 +766,9 @@ int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const 
                    long lda2, int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha,
                    const void* bias, const void* resid, long ldr, void* out, long ldo, void* out2, long ldo2,
                    int pre_rows, const void* aux, long ldaux, int group_m, hipStream_t st);
+int pso_gemm8p160_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
+                      int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
+                      const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 static int g_gemm_variant = 0;
@@ -821,17 +824,24 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // epilogue, LoRA K-tail, bias / alpha / residual.  Default for N >= 2560 with >= 256 tiles (tools/gemm8_ab.py, one
   // box: q/k/v 16384 x 3840 x 1280 1071 vs 937 TF/s, ff.out dX 8192 x 5120 x 1280 991 vs 945); N = 1280 keeps 128x160
   // (1.25 rounds of 256x256 tiles at M = 16384: 805 vs 928).  Variant 30 forces it, 31 keeps it off everywhere.
-  const bool ok8 = !g.conv.mode && !g.rowbias && g.out_dtype == PSO_BF16 && !g.accumulate && (g.N % 256) == 0 &&
-                   (g.K1 % 64) == 0 && al16(g.a1) && al16(g.b1) && (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 &&
-                   al16(g.out) && (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
-                   (!g.bias || al8(g.bias)) && fits30(g.M, g.lda1) && fits30(g.N, g.ldb1) &&
-                   (!g.a2 || ((g.tail_group_n == 0 || (g.tail_group_n % 256) == 0) && fits30(g.tail_m, g.lda2) &&
-                              fits30(g.N, g.ldb2)));
+  const bool base8 = !g.conv.mode && !g.rowbias && g.out_dtype == PSO_BF16 && !g.accumulate && (g.K1 % 64) == 0 &&
+                     al16(g.a1) && al16(g.b1) && (g.lda1 % 8) == 0 && (g.ldb1 % 8) == 0 && al16(g.out) &&
+                     (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
+                     (!g.bias || al8(g.bias)) && fits30(g.M, g.lda1) && fits30(g.N, g.ldb1) &&
+                     (!g.a2 || (fits30(g.tail_m, g.lda2) && fits30(g.N, g.ldb2)));
+  const bool ok8 = base8 && (g.N % 256) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 256) == 0);
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
   if (ok8 && (gv == 30 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);
+  // 8-phase 256 x 160 (gemm8p.hip) for the N % 160 == 0 widths with at least one round of tiles; variant 37 keeps the
+  // 2-phase 128 x 160, 38 forces the 8-phase form wherever it applies
+  const bool ok160 = base8 && (g.N % 160) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
+  const long t160 = (long)((g.M + 255) / 256) * (g.N / 160);
+  if (ok160 && (gv == 38 || (gv == 0 && t160 >= 256)))
+    return pso_gemm8p160_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
+                             g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);

@@ -84,18 +84,35 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 // its partner's fragment-read / staging segment (ping-pong).  Every phase then retires its own fragment reads
 // (lgkmcnt(0)) before its first barrier: with the lag, a partner may restage an image one barrier after that point.
 // SPRIO: waves 4-7 hold s_setprio 1 for the whole main loop instead of every wave raising it around its MFMAs.
-template <int EPI, bool STAG, bool SPRIO, bool FP8 = false>
+//
+// BN = 160 (256 x 160 tiles, every SDXL width N % 160 == 0 -- N = 1280 at M = 16384 is 512 tiles = 2 whole rounds where
+// 256 x 256 leaves 1.25): B half-tiles are 80 rows (10 glds pieces, staged by waves 0-4; the counted waits of waves 5-7
+// count their A pieces only), the quadrant is 128 x 80 with the 8 waves stacked along M (16 rows x 80 columns = 5 MFMA
+// tiles each), and the epilogue tile sits in LDS with a 336-B row pitch.  Plain epilogue only, bf16 only.
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
+  static_assert(BN == 256 || (BN == 160 && EPI == EPI8_NONE && !FP8), "256 x 160 tiles: plain bf16 epilogue only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
-  extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1][HT]
+  constexpr int BH = BN / 2;              // rows of a B half-tile image
+  constexpr int WRN = BN == 256 ? 4 : 8;  // waves along M inside a quadrant (x 8 / WRN along N)
+  constexpr int RW = 128 / WRN;           // rows per wave per quadrant
+  constexpr int MI = RW / 16;             // row subtiles per wave
+  constexpr int CW = BH / (8 / WRN);      // columns per wave per quadrant
+  constexpr int NJ = CW / 16;             // column subtiles per wave
+  constexpr int BHT = BH * 64;            // elements of a B half-tile image
+  constexpr int BUFE = 2 * HT + 2 * BHT;  // elements of one K-tile buffer [A0 A1 B0 B1]
+  constexpr int BPW = BH / 8 / 2;         // waves staging a B half-tile (2 pieces each): 8 or 5
+  extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1]
   const int tid = threadIdx.x, lane = tid & 63;
   // wave index in an SGPR: the LDS-DMA destinations (M0) are then scalar arithmetic, not 8 spilled VGPR addresses
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;  // 4 (M) x 2 (N) inside a quadrant
+  const int wr = wave / (8 / WRN), wc = wave % (8 / WRN);  // WRN (M) x 8/WRN (N) inside a quadrant
   const int fr = lane & 15, fk = lane >> 4;
+  // element offset of image img = buf * 4 + {A0 0, A1 1, B0 2, B1 3}
+  auto img_off = [](int img) { const int p = img & 3; return (img >> 2) * BUFE + (p < 2 ? p * HT : 2 * HT + (p - 2) * BHT); };
 
-  const int nbn = g.N / 256, nbm = (g.M + 255) / 256;
+  const int nbn = g.N / BN, nbm = (g.M + 255) / 256;
   const int nblk = nbn * nbm;
   int bid = blockIdx.x;
   {
@@ -112,7 +129,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     bm = first_m + in % gsz;
     bn = in / gsz;
   }
-  const int m0 = bm * 256, n0 = bn * 256;
+  const int m0 = bm * 256, n0 = bn * BN;
   const int nt1 = g.K / KT;  // K % KT == 0 (host-checked)
   // the LoRA K-tail: tiles made only of rows >= tail_m (the reference half of a paired pass) skip it (zero there)
   const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + KT - 1) / KT : 0;
@@ -132,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       const int R = (wave * 2 + i) * 8 + prow;
       const int lc = pch ^ (R & 7);
       aoff[h][i] = (unsigned)(min(m0 + h * 128 + R, g.M - 1) * (int)g.lda * ES + lc * 16);
-      woff[h][i] = (unsigned)((n0 + h * 128 + R) * (int)g.ldw * ES + lc * 16);
+      woff[h][i] = (unsigned)((n0 + h * BH + min(R, BH - 1)) * (int)g.ldw * ES + lc * 16);
     }
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
@@ -146,7 +163,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // image index = buf * 4 + {A0 0, A1 1, B0 2, B1 3}
   auto stage = [&](int kt, int img) {
     const int half = img & 3;
-    bf16_t* dst = l8 + img * HT + wave * 2 * 8 * 64;
+    bf16_t* dst = l8 + img_off(img) + wave * 2 * 8 * 64;
+    if (BPW < 8 && half >= 2 && wave >= BPW) return;  // 80-row B image: 10 pieces, waves 0-4
     if (kt < nt1) {
       const unsigned k0 = (unsigned)kt * 128u;  // bytes
       if (half < 2) {
@@ -162,7 +180,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int R = (half & 1) * 128 + (wave * 2 + i) * 8 + prow;
+        const int R = (half & 1) * (half < 2 ? 128 : BH) + (wave * 2 + i) * 8 + prow;
         unsigned off;
         if (half < 2) {
           const int m = m0 + R;
@@ -176,17 +194,17 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     }
   };
 
-  f32x4 acc[2][2][2][4];  // [A half][B half][row subtile][col subtile]
+  f32x4 acc[2][2][MI][NJ];  // [A half][B half][row subtile][col subtile]
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 af[2][2], bfr[4][2];  // [row subtile][kk], [col subtile][kk]  (bf16 form)
+  bf16x8 af[MI][2], bfr[NJ][2];  // [row subtile][kk], [col subtile][kk]  (bf16 form)
   i32x8 af8[2], bf8[4];         // FP8 form: [row subtile], [col subtile], 32 fp8 k per lane (two 16-B reads)
   // Fragment addresses: the swizzle term depends only on fr & 7, so within an image a lane needs one byte offset per
   // kk (subtiles are +2048-B immediates).  The image base is added per read by a volatile v_add: left to itself the
@@ -200,18 +218,18 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   for (int kk = 0; kk < 2; ++kk) {
     // bf16: 8-element chunk kk*4 + fk (k = 32 kk + 8 fk ..); fp8: the lane's 32 consecutive k are chunks 2 fk, 2 fk + 1
     const int ch = FP8 ? 2 * fk + kk : kk * 4 + fk;
-    la[kk] = (unsigned)swz8(wr * 32 + fr, ch) * 2u;
-    lb[kk] = (unsigned)swz8(wc * 64 + fr, ch) * 2u;
+    la[kk] = (unsigned)swz8(wr * RW + fr, ch) * 2u;
+    lb[kk] = (unsigned)swz8(wc * CW + fr, ch) * 2u;
   }
   i32x4_t ta[2], tb[4];
   auto read_a = [&](int img) {
-    const unsigned ib = l8base + (unsigned)(img * HT * 2);
+    const unsigned ib = l8base + (unsigned)(img_off(img) * 2);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned ad;
       asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(la[kk]));
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < MI; ++i) {
         if constexpr (FP8) {
           if (kk == 0) ta[i] = *(lds_frag4*)(uintptr_t)(ad + i * 2048);
           else af8[i] = __builtin_shufflevector(ta[i], *(lds_frag4*)(uintptr_t)(ad + i * 2048), 0, 1, 2, 3, 4, 5, 6, 7);
@@ -222,13 +240,13 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     }
   };
   auto read_b = [&](int img) {
-    const unsigned ib = l8base + (unsigned)(img * HT * 2);
+    const unsigned ib = l8base + (unsigned)(img_off(img) * 2);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned ad;
       asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb[kk]));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         if constexpr (FP8) {
           if (kk == 0) tb[j] = *(lds_frag4*)(uintptr_t)(ad + j * 2048);
           else bf8[j] = __builtin_shufflevector(tb[j], *(lds_frag4*)(uintptr_t)(ad + j * 2048), 0, 1, 2, 3, 4, 5, 6, 7);
@@ -291,13 +309,19 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[ha][hb][i][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
     }
     if (!SPRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  // the counted wait that retires all but the last three stagings (A, B, A or B, A, B pieces): 6 loads per wave, 2 for
+  // the waves that stage no B pieces (80-row B images)
+  auto vm_wait6 = [&]() {
+    if (BPW == 8 || wave < BPW) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   };
   // one phase: reads (RA / RB: which operand image to (re)load), the stage (if its K-tile exists), the optional
   // counted wait (VM: -1 none, else vmcnt(VM)), barrier, MFMAs of quadrant (HA, HB), barrier.
@@ -307,7 +331,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     if (RA) read_a((BUF) * 4 + (HA));                                                         \
     if ((STAGE_KT) < nt) stage((STAGE_KT), (STAGE_IMG));                                      \
     if (STAG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
-    if ((VM) == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");                           \
+    if ((VM) == 6) vm_wait6();                                                                \
     else if ((VM) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                      \
     __builtin_amdgcn_s_barrier();                                                             \
     __builtin_amdgcn_sched_barrier(0);                                                        \
@@ -319,7 +343,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // prologue: K-tile 0 -> E (in the steady-state staging order), K-tile 1 -> O.B0 O.A1 O.B1; wait for K-tile 0
   stage(0, 2); stage(0, 1); stage(0, 3); stage(0, 0);
   if (nt > 1) { stage(1, 6); stage(1, 5); stage(1, 7); }
-  if (nt > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if (nt > 1) vm_wait6();
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (STAG && wave >= 4) __builtin_amdgcn_s_barrier();
@@ -353,11 +377,62 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+          for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
     return;
   }
+  if constexpr (BN == 160) {
+    // 256 x 160 tile through LDS at a 168-element (336-B) row pitch: the ds_write_b64 of a 16-row fragment column hits
+    // 16 distinct bank pairs (84 dwords per row), rows are read back as 20 16-B chunks and stored whole (320 B)
+    __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
+    constexpr int TP = 168;
+    bf16_t* tl = l8;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      float bv[NJ][4];
+#pragma unroll
+      for (int jt = 0; jt < NJ; ++jt) {
+        const int n = n0 + hb * BH + jt * 16 + fk * 4;
+        const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
+        bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
+        bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
+      }
+#pragma unroll
+      for (int ha = 0; ha < 2; ++ha) {
+        const int R = ha * 128 + wr * 16 + fr;
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt) {
+          const int col = hb * BH + jt * 16 + fk * 4;
+          const f32x4 a = acc[ha][hb][0][jt];
+          const float al = g.alpha;
+          *reinterpret_cast<uint2*>(tl + R * TP + col) =
+              make_uint2(pack2bf(a[0] * al + bv[jt][0], a[1] * al + bv[jt][1]),
+                         pack2bf(a[2] * al + bv[jt][2], a[3] * al + bv[jt][3]));
+        }
+      }
+    }
+    __syncthreads();
+    const bool has_r = g.resid != nullptr;
+#pragma unroll 2
+    for (int p = 0; p < 10; ++p) {  // 256 rows x 20 chunks = 10 passes of 512
+      const int idx = p * 512 + tid;
+      const int R = idx / 20, c = idx - R * 20, m = m0 + R;
+      if (m >= g.M) continue;
+      uint4 y = *reinterpret_cast<const uint4*>(tl + R * TP + c * 8);
+      if (has_r) {  // residual added to the bf16-rounded projection (the unfused Linear + add)
+        const uint4 rv = *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + c * 8);
+        const uint32_t yw[4] = {y.x, y.y, y.z, y.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = pack2bf(bf2f(yw[e] & 0xffff) + bf2f(rw[e] & 0xffff), bf2f(yw[e] >> 16) + bf2f(rw[e] >> 16));
+        y = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + c * 8) = y;
+    }
+    return;
+  } else {
   // Epilogue through LDS: the operand ring (128 KB, free once the last phase's barrier has passed and no staging is
   // in flight) holds the whole 256 x 256 tile as bf16 (acc + bias, rounded once -- the unfused Linear's output),
   // then every wave stores whole 512-B rows in 16-B chunks (full 128-B lines per instruction) instead of the MFMA
@@ -473,21 +548,23 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + cq * 8) = y;
     }
   }
+  }  // BN == 256
 }
 
-template <int EPI, bool STAG, bool SPRIO, bool FP8 = false>
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 int launch8(const Gemm8Args& g, hipStream_t st) {
-  const int nblk = ((g.M + 255) / 256) * (g.N / 256);
-  const size_t shm = 8 * HT * sizeof(bf16_t);  // 128 KiB
+  const int nblk = ((g.M + 255) / 256) * (g.N / BN);
+  const size_t shm = (4 * HT + 4 * (BN / 2) * 64) * sizeof(bf16_t);  // 2 K-tile buffers: 128 KiB (256 x 256) / 104 KiB (256 x 160)
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8>,
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
   if (FP8) pso_note_kernel("gemm8p_kernel<%d, true, false, true>", EPI);
+  else if (BN == 160) pso_note_kernel("gemm8p_kernel<0, true, false, false, 160>");
   else pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
-  gemm8p_kernel<EPI, STAG, SPRIO, FP8><<<nblk, 512, shm, st>>>(g);
+  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN><<<nblk, 512, shm, st>>>(g);
   return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
 }
 
@@ -527,6 +604,20 @@ int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const 
   if (epi == EPI8_GEGLU) return launch8s<EPI8_GEGLU>(g, st, g_mode8);
   if (epi == EPI8_GEGLU_BWD) return launch8s<EPI8_GEGLU_BWD>(g, st, g_mode8);
   return launch8s<EPI8_NONE>(g, st, g_mode8);
+}
+
+// 256 x 160 tiles (N % 160 == 0, K % 64 == 0, plain epilogue; preconditions checked in gemm.hip)
+int pso_gemm8p160_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
+                      int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
+                      const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st) {
+  Gemm8Args g{};
+  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
+  g.M = M; g.N = N; g.K = K;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0; g.w2 = (const bf16_t*)w2; g.ldw2 = ldw2;
+  g.tail_m = tail_m; g.tail_group_n = a2 ? tail_group_n : 0;
+  g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  return launch8<EPI8_NONE, true, false, false, 160>(g, st);
 }
 
 // FP8 form (pso_amd.h, pso_gemm_fp8): staggered wave groups, epilogue 0 (bias / alpha / residual) or 1 (GEGLU)

@@ -182,7 +182,7 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 30, 31, 41])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 30, 31, 37, 38, 41])
 @pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
                                         (8192, 640, 320, 0), (1000, 700, 136, 0)])
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
@@ -263,6 +263,43 @@ def test_gemm_8phase_lora_tail_paired_resid(cuda, M, N, K, K2, group, tail_rows)
         K_.gemm(a, w, bias=b, resid=r, a2=u, w2=w2, alpha=0.75, tail_group_n=group, tail_rows=tail_rows, out=out)
         assert _rel(out, ref) < 4e-3
         assert _rel(out[tr:], ref[tr:]) < 4e-3 if tr < M else True
+        assert (sentinel[M:] == 7.0).all()
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (1000, 640, 640, 32, 640, 0),
+                                                      (4100, 1920, 640, 32, 640, 2048), (300, 320, 192, 0, 0, 0),
+                                                      (8192, 1280, 5120, 32, 0, 4096), (257, 640, 64, 96, 320, 100)])
+def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
+    """The 8-phase 256 x 160 kernel (gemm8p.hip BN = 160, variant 38): bias / alpha / residual epilogue, ragged last
+    row tile, odd / even K-tile counts (1..80), the LoRA K-tail grouped per 160-multiple column block or plain,
+    restricted to the first tail_rows rows; nothing is written past the output rows."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(38)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K + K2)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        b = torch.randn(N, device=cuda, generator=g).bfloat16()
+        r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+        y = a.float() @ w.float().t()
+        kw = {}
+        if K2:
+            tr = tail_rows or M
+            ng = N // group if group else 1
+            u = torch.randn(tr, K2 * ng, device=cuda, generator=g).bfloat16()
+            w2 = (torch.randn(N, K2, device=cuda, generator=g) / 6).bfloat16()
+            for j in range(ng):
+                cs = slice(j * group, (j + 1) * group) if group else slice(0, N)
+                y[:tr, cs] += u[:, K2 * j:K2 * (j + 1)].float() @ w2[cs].float().t()
+            kw = dict(a2=u, w2=w2, tail_group_n=group, tail_rows=tail_rows)
+        ref = (0.75 * y + b.float()).bfloat16().float() + r.float()
+        sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+        out = sentinel[:M]
+        K_.gemm(a, w, bias=b, resid=r, alpha=0.75, out=out, **kw)
+        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 160>"
+        assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
     finally:
         K_.lib().pso_gemm_set_variant(0)
