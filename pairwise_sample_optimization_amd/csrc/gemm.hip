@@ -781,7 +781,9 @@ static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automati
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
-  const int gv = gv_raw == 41 ? 0 : gv_raw;  // 41 = automatic dispatch with the per-lane epilogue
+  // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
+  // off / forced
+  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38) ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
@@ -835,11 +837,14 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);
-  // 8-phase 256 x 160 (gemm8p.hip) for the N % 160 == 0 widths with at least one round of tiles; variant 37 keeps the
-  // 2-phase 128 x 160, 38 forces the 8-phase form wherever it applies
+  // 8-phase 256 x 160 (gemm8p.hip) for the N % 160 == 0 widths with at least one round of tiles and a long reduction
+  // (K >= 2560: ff.out 16384 x 1280 x 5120 972 vs 942 TF/s, 32768 x 640 x 5120 1039 vs 910, 65536 x 640 x 2560 823
+  // vs 770); at K = 640 / 1280 the 2-phase 128 x 160 with two co-resident blocks per CU (one block's epilogue beside
+  // the other's main loop) stays ahead (16384 x 1280 x 1280 827 vs 724, tools/shape_prof.py one box).  Variant 37
+  // keeps the 2-phase 128 x 160, 38 forces the 8-phase form wherever it applies.
   const bool ok160 = base8 && (g.N % 160) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
   const long t160 = (long)((g.M + 255) / 256) * (g.N / 160);
-  if (ok160 && (gv == 38 || (gv == 0 && t160 >= 256)))
+  if (ok160 && gv_raw != 37 && (gv_raw == 38 || (gv == 0 && t160 >= 256 && Ktot >= 2560)))
     return pso_gemm8p160_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
