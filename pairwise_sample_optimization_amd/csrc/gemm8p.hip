@@ -33,6 +33,8 @@
 // accumulator is in true units and the epilogues are the bf16 form's.
 #include "common.h"
 
+#include <cstdlib>
+
 #define EPI8_NONE 0
 #define EPI8_GEGLU 1
 #define EPI8_GEGLU_BWD 2
@@ -114,7 +116,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 
   const int nbn = g.N / BN, nbm = (g.M + 255) / 256;
   const int nblk = nbn * nbm;
-  int bid = blockIdx.x;
+  // persistent: gridDim.x <= 256 workgroups (one per CU) walk the tiles; a tile's epilogue stores drain while the
+  // next tile's first K-tiles are in flight (a fresh workgroup per tile paid both latencies in series)
+  // (BN = 160 only: the 256 x 256 form spills ~30 VGPRs around a tile loop and runs its body once)
+  for (int tile = blockIdx.x; tile < nblk; tile += gridDim.x) {
+  int bid = tile;
   {
     const int q = nblk / 8, r = nblk % 8, x = bid % 8;
     if (nblk >= 8) bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
-    return;
+    goto tile_end;
   }
   if constexpr (BN == 160) {
     // 256 x 160 tile through LDS at a 168-element (336-B) row pitch: the ds_write_b64 of a 16-row fragment column hits
@@ -431,7 +437,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       }
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + c * 8) = y;
     }
-    return;
   } else {
   // Epilogue through LDS: the operand ring (128 KB, free once the last phase's barrier has passed and no staging is
   // in flight) holds the whole 256 x 256 tile as bf16 (acc + bias, rounded once -- the unfused Linear's output),
@@ -549,7 +554,20 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     }
   }
   }  // BN == 256
+  tile_end:
+  if constexpr (BN != 160) break;
+  // every wave's epilogue LDS reads retired before the next tile's staging overwrites the ring (no vmcnt wait: the
+  // stores keep draining)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }  // tiles
 }
+
+// persistent grid: one workgroup per CU (256 on MI355X; a multiple of 8 keeps every tile of a workgroup on its XCD)
+// (benchmark knob PSO_GEMM8_GRID: a larger value = one workgroup per tile)
+static const int g_grid8 = [] {
+  const char* e = getenv("PSO_GEMM8_GRID");
+  return e ? atoi(e) : 256;
+}();
 
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 int launch8(const Gemm8Args& g, hipStream_t st) {
@@ -564,7 +582,7 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
   if (FP8) pso_note_kernel("gemm8p_kernel<%d, true, false, true>", EPI);
   else if (BN == 160) pso_note_kernel("gemm8p_kernel<0, true, false, false, 160>");
   else pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
-  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN><<<nblk, 512, shm, st>>>(g);
+  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(g);
   return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
 }
 

@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILY = ("gemm_bf16_kernel", "gemm_tn", "gemm_skinny")
+FAMILY = ("gemm_bf16_kernel", "gemm8p_kernel", "gemm_tn", "gemm_skinny")
 
 
 def short(name):

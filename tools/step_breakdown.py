@@ -5,7 +5,7 @@ import csv
 import sys
 from collections import defaultdict
 
-FAMILY = ("gemm_bf16_kernel", "gemm_tn", "gemm_skinny")
+FAMILY = ("gemm_bf16_kernel", "gemm8p_kernel", "gemm_tn", "gemm_skinny")
 
 
 def short(name):
