@@ -19,6 +19,8 @@
 // recomputing P from Q, K and the saved LSE; delta = rowsum(dO * O) comes from a small pre-pass.
 #include "common.h"
 
+#include <type_traits>
+
 #define ATT_D 64
 #define ATT_KT 64  // keys per tile
 #define ATT_THREADS 256
@@ -818,7 +820,10 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     const bf16_t* sKt = sRing[kt % STG][1];
     const bf16_t* sVr = sRing[kt % STG][2];
     const int kbase = kt * ATT_KT;
-    const bool kpart = kbase + ATT_KT > a.Sk;  // wave-uniform
+    // the tile body in two straight-line forms: the key mask of a partial last tile is decided once per tile, not
+    // per (key block, query block) -- a branch there splits the body into 16 blocks the scheduler cannot interleave
+    auto body = [&](auto KPART_) {
+    constexpr bool kpart = decltype(KPART_)::value;
     f32x4 dsT[2][4];  // lane holds dS[q = qi*16 + c][key = kj*16 + 4g + r]
 #pragma unroll
     for (int kj = 0; kj < 4; ++kj) {
@@ -836,7 +841,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
         sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[1], qf[qi][1], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[0], of[qi][0], pacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[1], of[qi][1], pacc, 0, 0, 0);
-        if (kpart) {  // last, partial key tile only: padded keys get p = 0
+        if constexpr (kpart) {  // last, partial key tile only: padded keys get p = 0
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = kbase + kj * 16 + 4 * g + r;
@@ -862,6 +867,9 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
         for (int qi = 0; qi < 2; ++qi) dq[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf[qi], dq[qi][dt], 0, 0, 0);
       }
     }
+    };
+    if (kbase + ATT_KT > a.Sk) body(std::true_type{});  // wave-uniform
+    else body(std::false_type{});
   }
   const float sc = a.scale_log2 * 0.69314718055994531f;
   bf16_t* DQ = a.dq + b * a.sdq_b + h * ATT_D;
