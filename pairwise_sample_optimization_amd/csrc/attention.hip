@@ -854,17 +854,31 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
         }
       }
     }
+    // K^T fragments by inline-asm transposed reads: the builtin form makes hipcc drain the LDS-DMA ring (vmcnt(0),
+    // the next two key tiles included) before them on every tile
+    s16x4 kr[2][8];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pf[2];
-#pragma unroll
-      for (int qi = 0; qi < 2; ++qi) pf[qi] = pack_p(dsT[qi][2 * ks], dsT[qi][2 * ks + 1]);
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 kf = cat_frag(tr_read(sKt, (2 * ks) * 16 + 4 * g, dt * 16, lane),
-                                   tr_read(sKt, (2 * ks + 1) * 16 + 4 * g, dt * 16, lane));
+        kr[ks][2 * dt] = tr_read_asm(sKt, (2 * ks) * 16 + 4 * g, dt * 16, lane);
+        kr[ks][2 * dt + 1] = tr_read_asm(sKt, (2 * ks + 1) * 16 + 4 * g, dt * 16, lane);
+      }
+    bf16x8 pf[2][2];
 #pragma unroll
-        for (int qi = 0; qi < 2; ++qi) dq[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf[qi], dq[qi][dt], 0, 0, 0);
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) pf[ks][qi] = pack_p(dsT[qi][2 * ks], dsT[qi][2 * ks + 1]);
+    lds_wait8(kr[0]);
+    lds_wait8(kr[1]);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 kf = cat_frag(kr[ks][2 * dt], kr[ks][2 * dt + 1]);
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi)
+          dq[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, pf[ks][qi], dq[qi][dt], 0, 0, 0);
       }
     }
     };
