@@ -88,31 +88,33 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 // SPRIO: waves 4-7 hold s_setprio 1 for the whole main loop instead of every wave raising it around its MFMAs.
 //
 // BN = 160 (256 x 160 tiles, every SDXL width N % 160 == 0 -- N = 1280 at M = 16384 is 512 tiles = 2 whole rounds where
-// 256 x 256 leaves 1.25): B half-tiles are 80 rows (10 glds pieces, staged by waves 0-4; the counted waits of waves 5-7
-// count their A pieces only), the quadrant is 128 x 80 with the 8 waves stacked along M (16 rows x 80 columns = 5 MFMA
-// tiles each), and the epilogue tile sits in LDS with a 336-B row pitch.  Plain epilogue only, bf16 only.
+// 256 x 256 leaves 1.25): the B tile splits into a 96-row and a 64-row image (12 / 8 glds pieces, staged by waves 0-5 /
+// 0-3; the counted waits of the other waves count only what they staged), so the quadrants are 128 x 96 and 128 x 64
+// with the waves 4 (M) x 2 (N) as in the 256 x 256 form (32 x 48 = 6 and 32 x 32 = 4 MFMA tiles per wave): per K-tile
+// 10 / 4 / 4 / 4 fragment reads against 12 / 12 / 8 / 8 MFMAs per phase.  The epilogue tile sits in LDS with a 336-B
+// row pitch.  Plain epilogue only, bf16 only.
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   static_assert(BN == 256 || (BN == 160 && EPI == EPI8_NONE && !FP8), "256 x 160 tiles: plain bf16 epilogue only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
-  constexpr int BH = BN / 2;              // rows of a B half-tile image
-  constexpr int WRN = BN == 256 ? 4 : 8;  // waves along M inside a quadrant (x 8 / WRN along N)
-  constexpr int RW = 128 / WRN;           // rows per wave per quadrant
-  constexpr int MI = RW / 16;             // row subtiles per wave
-  constexpr int CW = BH / (8 / WRN);      // columns per wave per quadrant
-  constexpr int NJ = CW / 16;             // column subtiles per wave
-  constexpr int BHT = BH * 64;            // elements of a B half-tile image
-  constexpr int BUFE = 2 * HT + 2 * BHT;  // elements of one K-tile buffer [A0 A1 B0 B1]
-  constexpr int BPW = BH / 8 / 2;         // waves staging a B half-tile (2 pieces each): 8 or 5
+  constexpr int BH0 = BN == 256 ? 128 : 96, BH1 = BN - BH0;  // rows of the two B images
+  constexpr int MI = 2;                                       // row subtiles per wave (32 rows of a 128-row half)
+  constexpr int CW0 = BH0 / 2, CW1 = BH1 / 2;                 // columns per wave in the B0 / B1 quadrants
+  constexpr int NJ0 = CW0 / 16, NJ1 = CW1 / 16, NJ = NJ0;     // column subtiles per wave
+  constexpr int BUFE = 2 * HT + BN * 64;                      // elements of one K-tile buffer [A0 A1 B0 B1]
+  constexpr int BW0 = BH0 / 16, BW1 = BH1 / 16;               // waves staging B0 / B1 (2 pieces each)
   extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1]
   const int tid = threadIdx.x, lane = tid & 63;
   // wave index in an SGPR: the LDS-DMA destinations (M0) are then scalar arithmetic, not 8 spilled VGPR addresses
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / (8 / WRN), wc = wave % (8 / WRN);  // WRN (M) x 8/WRN (N) inside a quadrant
+  const int wr = wave >> 1, wc = wave & 1;  // 4 (M) x 2 (N) inside a quadrant
   const int fr = lane & 15, fk = lane >> 4;
   // element offset of image img = buf * 4 + {A0 0, A1 1, B0 2, B1 3}
-  auto img_off = [](int img) { const int p = img & 3; return (img >> 2) * BUFE + (p < 2 ? p * HT : 2 * HT + (p - 2) * BHT); };
+  auto img_off = [](int img) {
+    const int p = img & 3;
+    return (img >> 2) * BUFE + (p < 2 ? p * HT : 2 * HT + (p - 2) * BH0 * 64);
+  };
 
   const int nbn = g.N / BN, nbm = (g.M + 255) / 256;
   const int nblk = nbn * nbm;
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       const int R = (wave * 2 + i) * 8 + prow;
       const int lc = pch ^ (R & 7);
       aoff[h][i] = (unsigned)(min(m0 + h * 128 + R, g.M - 1) * (int)g.lda * ES + lc * 16);
-      woff[h][i] = (unsigned)((n0 + h * BH + min(R, BH - 1)) * (int)g.ldw * ES + lc * 16);
+      woff[h][i] = (unsigned)((n0 + h * BH0 + min(R, (h ? BH1 : BH0) - 1)) * (int)g.ldw * ES + lc * 16);
     }
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   auto stage = [&](int kt, int img) {
     const int half = img & 3;
     bf16_t* dst = l8 + img_off(img) + wave * 2 * 8 * 64;
-    if (BPW < 8 && half >= 2 && wave >= BPW) return;  // 80-row B image: 10 pieces, waves 0-4
+    if (BN != 256 && half >= 2 && wave >= (half == 2 ? BW0 : BW1)) return;  // 96 / 64-row B images: waves 0-5 / 0-3
     if (kt < nt1) {
       const unsigned k0 = (unsigned)kt * 128u;  // bytes
       if (half < 2) {
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int R = (half & 1) * (half < 2 ? 128 : BH) + (wave * 2 + i) * 8 + prow;
+        const int R = (half & 1) * (half < 2 ? 128 : BH0) + (wave * 2 + i) * 8 + prow;
         unsigned off;
         if (half < 2) {
           const int m = m0 + R;
@@ -224,8 +226,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   for (int kk = 0; kk < 2; ++kk) {
     // bf16: 8-element chunk kk*4 + fk (k = 32 kk + 8 fk ..); fp8: the lane's 32 consecutive k are chunks 2 fk, 2 fk + 1
     const int ch = FP8 ? 2 * fk + kk : kk * 4 + fk;
-    la[kk] = (unsigned)swz8(wr * RW + fr, ch) * 2u;
-    lb[kk] = (unsigned)swz8(wc * CW + fr, ch) * 2u;
+    la[kk] = (unsigned)swz8(wr * 32 + fr, ch) * 2u;
+    lb[kk] = (unsigned)swz8(fr, ch) * 2u;  // + the wave's column offset wc * CW rows (a multiple of 8: same swizzle)
   }
   i32x4_t ta[2], tb[4];
   auto read_a = [&](int img) {
@@ -245,14 +247,15 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       }
     }
   };
-  auto read_b = [&](int img) {
-    const unsigned ib = l8base + (unsigned)(img_off(img) * 2);
+  auto read_b = [&](auto HB_, int buf) {
+    constexpr int hb = decltype(HB_)::value;
+    const unsigned ib = l8base + (unsigned)(img_off(buf * 4 + 2 + hb) * 2) + (unsigned)(wc * (hb ? CW1 : CW0) * 128);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned ad;
       asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb[kk]));
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
+      for (int j = 0; j < (hb ? NJ1 : NJ0); ++j) {
         if constexpr (FP8) {
           if (kk == 0) tb[j] = *(lds_frag4*)(uintptr_t)(ad + j * 2048);
           else bf8[j] = __builtin_shufflevector(tb[j], *(lds_frag4*)(uintptr_t)(ad + j * 2048), 0, 1, 2, 3, 4, 5, 6, 7);
@@ -317,23 +320,24 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j)
+          for (int j = 0; j < (hb ? NJ1 : NJ0); ++j)
             acc[ha][hb][i][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
     }
     if (!SPRIO) __builtin_amdgcn_s_setprio(0);
   };
-  // the counted wait that retires all but the last three stagings (A, B, A or B, A, B pieces): 6 loads per wave, 2 for
-  // the waves that stage no B pieces (80-row B images)
+  // the counted wait that retires all but the last three stagings (B0, A1, B1): 6 loads per wave, fewer for the waves
+  // that stage no B1 (4) or no B pieces at all (2) in the 256 x 160 form
   auto vm_wait6 = [&]() {
-    if (BPW == 8 || wave < BPW) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (BN == 256 || wave < BW1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (wave < BW0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   };
   // one phase: reads (RA / RB: which operand image to (re)load), the stage (if its K-tile exists), the optional
   // counted wait (VM: -1 none, else vmcnt(VM)), barrier, MFMAs of quadrant (HA, HB), barrier.
 #define PHASE(BUF, HA, HB, RA, RB, STAGE_KT, STAGE_IMG, VM)                                   \
   {                                                                                           \
-    if (RB) read_b((BUF) * 4 + 2 + (HB));                                                     \
+    if (RB) read_b(ic8<(HB)>{}, (BUF));                                                       \
     if (RA) read_a((BUF) * 4 + (HA));                                                         \
     if ((STAGE_KT) < nt) stage((STAGE_KT), (STAGE_IMG));                                      \
     if (STAG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+          for (int j = 0; j < (b ? NJ1 : NJ0); ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
     goto tile_end;
   }
   if constexpr (BN == 160) {
@@ -394,30 +398,35 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
     constexpr int TP = 168;
     bf16_t* tl = l8;
+    auto epi_half = [&](auto HB_) {
+      constexpr int hb = decltype(HB_)::value, nj = hb ? NJ1 : NJ0;
+      const int c0 = hb * BH0 + wc * (hb ? CW1 : CW0);
+      float bv[nj][4];
 #pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-      float bv[NJ][4];
-#pragma unroll
-      for (int jt = 0; jt < NJ; ++jt) {
-        const int n = n0 + hb * BH + jt * 16 + fk * 4;
+      for (int jt = 0; jt < nj; ++jt) {
+        const int n = n0 + c0 + jt * 16 + fk * 4;
         const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
         bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
         bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
       }
 #pragma unroll
-      for (int ha = 0; ha < 2; ++ha) {
-        const int R = ha * 128 + wr * 16 + fr;
+      for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
-        for (int jt = 0; jt < NJ; ++jt) {
-          const int col = hb * BH + jt * 16 + fk * 4;
-          const f32x4 a = acc[ha][hb][0][jt];
-          const float al = g.alpha;
-          *reinterpret_cast<uint2*>(tl + R * TP + col) =
-              make_uint2(pack2bf(a[0] * al + bv[jt][0], a[1] * al + bv[jt][1]),
-                         pack2bf(a[2] * al + bv[jt][2], a[3] * al + bv[jt][3]));
+        for (int i = 0; i < MI; ++i) {
+          const int R = ha * 128 + wr * 32 + i * 16 + fr;
+#pragma unroll
+          for (int jt = 0; jt < nj; ++jt) {
+            const int col = c0 + jt * 16 + fk * 4;
+            const f32x4 a = acc[ha][hb][i][jt];
+            const float al = g.alpha;
+            *reinterpret_cast<uint2*>(tl + R * TP + col) =
+                make_uint2(pack2bf(a[0] * al + bv[jt][0], a[1] * al + bv[jt][1]),
+                           pack2bf(a[2] * al + bv[jt][2], a[3] * al + bv[jt][3]));
+          }
         }
-      }
-    }
+    };
+    epi_half(ic8<0>{});
+    epi_half(ic8<1>{});
     __syncthreads();
     const bool has_r = g.resid != nullptr;
 #pragma unroll 2
