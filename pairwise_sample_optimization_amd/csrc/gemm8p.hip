@@ -398,6 +398,15 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
     constexpr int TP = 168;
     bf16_t* tl = l8;
+    // the residual chunks of all 10 store passes are requested first: their latency runs under the LDS staging
+    const bool has_r = g.resid != nullptr;
+    uint4 rvp[10];
+#pragma unroll
+    for (int p = 0; p < 10; ++p) {
+      const int idx = p * 512 + tid;
+      const int R = idx / 20, c = idx - R * 20, m = min(m0 + R, g.M - 1);
+      rvp[p] = has_r ? *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + c * 8) : make_uint4(0, 0, 0, 0);
+    }
     auto epi_half = [&](auto HB_) {
       constexpr int hb = decltype(HB_)::value, nj = hb ? NJ1 : NJ0;
       const int c0 = hb * BH0 + wc * (hb ? CW1 : CW0);
@@ -427,16 +436,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     };
     epi_half(ic8<0>{});
     epi_half(ic8<1>{});
-    __syncthreads();
-    const bool has_r = g.resid != nullptr;
-#pragma unroll 2
+    // LDS-only barrier: the residual loads stay in flight across it (__syncthreads would wait for them)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
     for (int p = 0; p < 10; ++p) {  // 256 rows x 20 chunks = 10 passes of 512
       const int idx = p * 512 + tid;
       const int R = idx / 20, c = idx - R * 20, m = m0 + R;
       if (m >= g.M) continue;
       uint4 y = *reinterpret_cast<const uint4*>(tl + R * TP + c * 8);
       if (has_r) {  // residual added to the bf16-rounded projection (the unfused Linear + add)
-        const uint4 rv = *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + c * 8);
+        const uint4 rv = rvp[p];
         const uint32_t yw[4] = {y.x, y.y, y.z, y.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
         uint32_t o[4];
 #pragma unroll
