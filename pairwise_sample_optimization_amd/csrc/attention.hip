@@ -351,7 +351,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, i
   constexpr int STG = 3;
   constexpr int PIECES = 4;
   __shared__ __attribute__((aligned(16))) bf16_t sKV[STG][2][ATT_KT * ATT_D];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA destinations (M0) are scalar
   const int g = lane >> 4, c = lane & 15;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int qb = bid % nqb, bh = bid / nqb;
@@ -564,7 +565,8 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
   extern __shared__ __attribute__((aligned(16))) bf16_t att_dyn[];
   bf16_t* const sbase = att_dyn;                                   // [STG][4][IMG]: Qr, Qt, Or, Ot
   float* const sLD = reinterpret_cast<float*>(att_dyn + STG * 4 * IMG);  // [STG][2][64]: LSE, delta
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA destinations (M0) and the LSE / delta resource are scalar
   const int g = lane >> 4, c = lane & 15;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_bh = nkb * a.q_split;
@@ -591,23 +593,40 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
   const int prow = lane >> 3, pch = lane & 7;
   const int lcR = pch ^ prow;                       // row-image source chunk
   const int lcT = pch ^ (2 * ((prow >> 1) & 3));    // transposed-image source chunk
+  // buffer_load ... lds against per-(batch, head) SGPR resources ending at query row Sq - 1 (rows past it read as
+  // zeros; padded queries are masked through the LSE): loop-invariant 32-bit lane offsets, the tile advance is the
+  // scalar soffset
+  const __amdgpu_buffer_rsrc_t rQ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)(((long)(a.Sq - 1) * a.ldq + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rO =
+      __builtin_amdgcn_make_buffer_rsrc((void*)DO, (short)0, (int)(((long)(a.Sq - 1) * a.lddo + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rL =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(wave == 0 ? LSE : DEL), (short)0, a.Sq * 4, 0x00020000);
+  unsigned qro[2], qto[2], oro[2], oto[2];
+#pragma unroll
+  for (int pw = 0; pw < 2; ++pw) {
+    const int row = (wave * 2 + pw) * 8 + prow;
+    qro[pw] = (unsigned)(row * (int)a.ldq + lcR * 8) * 2u;
+    qto[pw] = (unsigned)(row * (int)a.ldq + lcT * 8) * 2u;
+    oro[pw] = (unsigned)(row * (int)a.lddo + lcR * 8) * 2u;
+    oto[pw] = (unsigned)(row * (int)a.lddo + lcT * 8) * 2u;
+  }
+  const int qstep = ATT_KT * (int)a.ldq * 2, ostep = ATT_KT * (int)a.lddo * 2;  // bytes per query tile
   auto issue = [&](int qt, int buf) {
     bf16_t* img = sbase + buf * 4 * IMG;
-    if (wave < 2) {  // LSE (wave 0) / delta (wave 1): one dword per lane, issued first so it retires first
-      const int q = min(qt * ATT_KT + lane, a.Sq - 1);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>((wave == 0 ? LSE : DEL) + q),
-                                       (att_lds_void*)(sLD + (buf * 2 + wave) * 64), 4, 0, 0);
-    }
+    if (wave < 2)  // LSE (wave 0) / delta (wave 1): one dword per lane, issued first so it retires first
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rL, (att_lds_void*)(sLD + (buf * 2 + wave) * 64), 4, lane * 4,
+                                               qt * ATT_KT * 4, 0, 0);
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw) {
       const int piece = wave * 2 + pw;
-      const int q = min(qt * ATT_KT + piece * 8 + prow, a.Sq - 1);  // clamped rows: masked through the LSE
-      const bf16_t* qrow = Q + (long)q * a.ldq;
-      const bf16_t* orow = DO + (long)q * a.lddo;
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(qrow + lcR * 8), (att_lds_void*)(img + piece * 8 * ATT_D), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(qrow + lcT * 8), (att_lds_void*)(img + IMG + piece * 8 * ATT_D), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(orow + lcR * 8), (att_lds_void*)(img + 2 * IMG + piece * 8 * ATT_D), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(orow + lcT * 8), (att_lds_void*)(img + 3 * IMG + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + piece * 8 * ATT_D), 16, qro[pw], qt * qstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + IMG + piece * 8 * ATT_D), 16, qto[pw], qt * qstep,
+                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rO, (att_lds_void*)(img + 2 * IMG + piece * 8 * ATT_D), 16, oro[pw],
+                                               qt * ostep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rO, (att_lds_void*)(img + 3 * IMG + piece * 8 * ATT_D), 16, oto[pw],
+                                               qt * ostep, 0, 0);
     }
   };
 
@@ -745,7 +764,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
   constexpr int PIECES = 6;  // glds per wave per tile: 2 pieces x 3 images
   constexpr int IMG = ATT_KT * ATT_D;
   __shared__ __attribute__((aligned(16))) bf16_t sRing[STG][3][IMG];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA destinations (M0) are scalar
   const int g = lane >> 4, c = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
   const int q0 = blockIdx.x * 128 + wave * 32;
@@ -794,18 +814,32 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
   const int prow = lane >> 3, pch = lane & 7;
   const int lcR = pch ^ prow;                     // row-image source chunk (swz_row)
   const int lcT = pch ^ (2 * ((prow >> 1) & 3));  // transposed-read image source chunk (swz_tr)
+  // buffer_load ... lds against per-(batch, head) SGPR resources ending at key row Sk - 1 (rows past it read as zeros
+  // and are masked on the last tile): the per-lane part of every staging address is a loop-invariant 32-bit offset and
+  // the tile advance the scalar soffset (per-lane 64-bit row pointers cost ~50 VALU instructions per tile)
+  const __amdgpu_buffer_rsrc_t rK =
+      __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, (int)(((long)(a.Sk - 1) * a.ldk + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV =
+      __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, (int)(((long)(a.Sk - 1) * a.ldv + ATT_D) * 2), 0x00020000);
+  unsigned kro[2], kto[2], vro[2];
+#pragma unroll
+  for (int pw = 0; pw < 2; ++pw) {
+    const int row = (wave * 2 + pw) * 8 + prow;
+    kro[pw] = (unsigned)(row * (int)a.ldk + lcR * 8) * 2u;
+    kto[pw] = (unsigned)(row * (int)a.ldk + lcT * 8) * 2u;
+    vro[pw] = (unsigned)(row * (int)a.ldv + lcR * 8) * 2u;
+  }
+  const int kstep = ATT_KT * (int)a.ldk * 2, vstep = ATT_KT * (int)a.ldv * 2;  // bytes per key tile
   auto issue = [&](int kt, int buf) {
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw) {
       const int piece = wave * 2 + pw;
-      const int key = min(kt * ATT_KT + piece * 8 + prow, a.Sk - 1);  // clamped rows are masked (p = 0)
-      const bf16_t* krow = K + (long)key * a.ldk;
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(krow + lcR * 8),
-                                       (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(krow + lcT * 8),
-                                       (att_lds_void*)(sRing[buf][1] + piece * 8 * ATT_D), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(V + (long)key * a.ldv + lcR * 8),
-                                       (att_lds_void*)(sRing[buf][2] + piece * 8 * ATT_D), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, kro[pw],
+                                               kt * kstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][1] + piece * 8 * ATT_D), 16, kto[pw],
+                                               kt * kstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (att_lds_void*)(sRing[buf][2] + piece * 8 * ATT_D), 16, vro[pw],
+                                               kt * vstep, 0, 0);
     }
   };
   issue(0, 0);

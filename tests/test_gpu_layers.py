@@ -84,6 +84,31 @@ def test_attention_fwd_bwd(cuda, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,Sq,Sk", [(2, 5, 300, 77), (1, 2, 100, 100), (1, 4, 130, 1000)])
+def test_attention_partial_tiles_poisoned_tail(cuda, B, H, Sq, Sk):
+    """Partial last key / query tiles with NaN in the memory right past the last row of Q, K, V and dO: the staging
+    loads of the forward, dQ and dK/dV kernels must never let a row past the end reach the arithmetic (0 * NaN)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(7 * Sq + Sk)
+
+    def poisoned(S):
+        buf = torch.full((B * S + 192, C), float("nan"), device=cuda, dtype=torch.bfloat16)
+        t = buf[:B * S]
+        t.copy_(torch.randn(B * S, C, device=cuda, generator=g).bfloat16())
+        return t.view(B, S, C)
+
+    q, k, v, do = poisoned(Sq), poisoned(Sk), poisoned(Sk), poisoned(Sq)
+    o, lse = K.attention_fwd(q, k, v, H)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, H)
+    assert torch.isfinite(o).all() and _rel(o, ref) < 1e-2
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    dq, dk, dv = K.attention_bwd(q, k, v, o, lse, do, H)
+    for got, want in ((dq, gq), (dk, gk), (dv, gv)):
+        assert torch.isfinite(got).all() and _rel(got, want) < 2e-2
+
+
 @pytest.mark.parametrize("variant", [2, 4])
 @pytest.mark.parametrize("B,H,Sq,Sk", [(2, 2, 256, 256), (2, 5, 300, 77), (1, 4, 130, 1000), (3, 20, 1024, 1024)])
 def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
