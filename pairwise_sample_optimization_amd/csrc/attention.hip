@@ -844,15 +844,17 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
   };
   issue(0, 0);
   if (nkt > 1) issue(1, 1);
-  for (int kt = 0; kt < nkt; ++kt) {
+  // the tile loop unrolled by the ring depth: every LDS fragment address is a lane base + an immediate
+  auto tile = [&](auto BUF_, int kt) {
+    constexpr int buf = decltype(BUF_)::value;
     // tile kt landed (all but this wave's PIECES youngest), then every wave's; the barrier also orders every wave's
     // reads of tile kt-1 before its buffer is re-staged below
     if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % STG);
-    const bf16_t* sKr = sRing[kt % STG][0];
-    const bf16_t* sKt = sRing[kt % STG][1];
-    const bf16_t* sVr = sRing[kt % STG][2];
+    if (kt + 2 < nkt) issue(kt + 2, (buf + 2) % STG);
+    const bf16_t* sKr = sRing[buf][0];
+    const bf16_t* sKt = sRing[buf][1];
+    const bf16_t* sVr = sRing[buf][2];
     const int kbase = kt * ATT_KT;
     // the tile body in two straight-line forms: the key mask of a partial last tile is decided once per tile, not
     // per (key block, query block) -- a branch there splits the body into 16 blocks the scheduler cannot interleave
@@ -918,6 +920,11 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     };
     if (kbase + ATT_KT > a.Sk) body(std::true_type{});  // wave-uniform
     else body(std::false_type{});
+  };
+  for (int kt = 0; kt < nkt; kt += STG) {
+    tile(ic<0>{}, kt);
+    if (kt + 1 < nkt) tile(ic<1>{}, kt + 1);
+    if (kt + 2 < nkt) tile(ic<2>{}, kt + 2);
   }
   const float sc = a.scale_log2 * 0.69314718055994531f;
   bf16_t* DQ = a.dq + b * a.sdq_b + h * ATT_D;
