@@ -254,8 +254,10 @@ def test_graph_epoch_equals_eager_epoch(cuda):
     # rounding difference on a near-zero gradient into up to ~lr of parameter change: bar 1 % of lr = 1e-5
     assert torch.allclose(u_e.lora.master, u_g.lora.master, rtol=0, atol=1e-5), \
         (u_e.lora.master - u_g.lora.master).abs().max().item()
+    # moments: the float-atomic dW sums differ in their last bits between the two runs, and where an element's sum
+    # cancels that difference is large RELATIVE to the element; bar it against the tensor's scale instead
     for a, b in ((tr_e.exp_avg, tr_g.exp_avg), (tr_e.exp_avg_sq, tr_g.exp_avg_sq)):
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-9), (a - b).abs().max().item()
+        assert (a - b).abs().max().item() <= 1e-4 * a.abs().max().item() + 1e-12, (a - b).abs().max().item()
 
 
 def test_full_unet_micro_step_vs_fp32_reference(cuda):
