@@ -75,7 +75,8 @@ struct AttnArgs {
   float scale_log2;            // softmax scale * log2(e)
   // backward
   const bf16_t* dO; long lddo; long sdo_b;
-  float* delta;                // [B][H][Sq]
+  float* delta;                // [B][H][Sq]: -rowsum(dO * O), written by the dQ kernel for the dK/dV kernel
+  float* lse2;                 // [B][H][Sq]: the LSE in log2 units, likewise (no per-tile rescale / negation there)
   bf16_t *dq, *dk, *dv; long lddq, lddk, lddv; long sdq_b, sdk_b, sdv_b;
   float *dk_acc, *dv_acc;      // fp32 [B][Sk][H*64] when q is split (cross-attention)
   int q_split;
@@ -579,9 +580,8 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
   const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
   const bf16_t* V = a.v + b * a.sv_b + h * ATT_D;
   const bf16_t* DO = a.dO + b * a.sdo_b + h * ATT_D;
-  const float* LSE = a.lse + ((long)b * a.H + h) * a.Sq;
-  const float* DEL = a.delta + ((long)b * a.H + h) * a.Sq;
-  const float ln2inv = 1.4426950408889634f;
+  const float* LSE = a.lse2 + ((long)b * a.H + h) * a.Sq;  // log2 units
+  const float* DEL = a.delta + ((long)b * a.H + h) * a.Sq;  // -delta
   const float c2 = a.scale_log2;
 
   const int nqt = (a.Sq + ATT_KT - 1) / ATT_KT;
@@ -682,8 +682,8 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         asm volatile("ds_read_b128 %0, %1" : "=v"(d4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // nothing reads l4 / d4 (or moves above) before the wait
-        float lq[4] = {l4.x * ln2inv, l4.y * ln2inv, l4.z * ln2inv, l4.w * ln2inv};
-        const float dq_[4] = {d4.x, d4.y, d4.z, d4.w};
+        float lq[4] = {l4.x, l4.y, l4.z, l4.w};  // LSE * log2(e), from the dQ kernel
+        const f32x4 ndel = {d4.x, d4.y, d4.z, d4.w};  // -delta, from the dQ kernel
         if (qpart) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 #pragma unroll
         for (int kj = 0; kj < KJ; ++kj) {
           // dP accumulates onto -delta (register r = query 4g + r), so dS = P * acc: one VALU op per score less
-          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {-dq_[0], -dq_[1], -dq_[2], -dq_[3]};
+          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = ndel;
           sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[0], kf[kj][0], sacc, 0, 0, 0);
           sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[1], kf[kj][1], sacc, 0, 0, 0);
           pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[0], vf[kj][0], pacc, 0, 0, 0);
@@ -801,8 +801,12 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     part += __shfl_xor(part, 32, 64);
     dl[qi] = part;
     lq[qi] = qr < a.Sq ? a.lse[((long)b * a.H + h) * a.Sq + qr] * ln2inv : INFINITY;
-    // published for the dK/dV kernel, which runs after this one on the stream
-    if (qr < a.Sq && g == 0) a.delta[((long)b * a.H + h) * a.Sq + qr] = part;
+    // published for the dK/dV kernel, which runs after this one on the stream: -delta and the LSE in log2 units, the
+    // forms its tile loop consumes as they stand
+    if (qr < a.Sq && g == 0) {
+      a.delta[((long)b * a.H + h) * a.Sq + qr] = -part;
+      a.lse2[((long)b * a.H + h) * a.Sq + qr] = lq[qi];
+    }
   }
   f32x4 dq[2][4];
 #pragma unroll
@@ -1025,7 +1029,7 @@ size_t pso_attention_bwd_ws_bytes(int B, int H, int Sq, int Sk) {
   size_t d = (size_t)B * H * Sq * sizeof(float);
   const int qs = cross_qsplit(B, H, Sq, Sk);
   size_t acc = qs > 1 ? 2 * (size_t)qs * B * Sk * H * ATT_D * sizeof(float) : 0;
-  return ((d + 255) / 256) * 256 + acc;
+  return 2 * (((d + 255) / 256) * 256) + acc;  // -delta, LSE * log2(e), split partials
 }
 
 int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
@@ -1045,11 +1049,13 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   a.o = (bf16_t*)o; a.ldo = ldo; a.so_b = so_b; a.lse = (float*)lse;
   a.Sq = Sq; a.Sk = Sk; a.H = H; a.scale_log2 = scale * 1.4426950408889634f;
   a.dO = (const bf16_t*)dO; a.lddo = lddo; a.sdo_b = sdo_b;
+  const size_t dsz = (((size_t)B * H * Sq * sizeof(float) + 255) / 256) * 256;
   float* delta = (float*)ws;
   a.delta = delta;
+  a.lse2 = (float*)((char*)ws + dsz);
   a.dq = (bf16_t*)dq; a.dk = (bf16_t*)dk; a.dv = (bf16_t*)dv;
   a.lddq = lddq; a.lddk = lddk; a.lddv = lddv; a.sdq_b = sdq_b; a.sdk_b = sdk_b; a.sdv_b = sdv_b;
-  const size_t doff = (((size_t)B * H * Sq * sizeof(float) + 255) / 256) * 256;
+  const size_t doff = 2 * dsz;
   const int nkb = cdiv(Sk, 128);
   const int qsplit = cross_qsplit(B, H, Sq, Sk);
   const long part = (long)B * Sk * H * ATT_D;  // elements of one split slice
