@@ -481,15 +481,13 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, i
       m = vmax3(m, s[qi][2][3], s[qi][3][0]);
       m = vmax3(m, s[qi][3][1], s[qi][3][2]);
       m = vmax2(m, s[qi][3][3]);
-      // growth test on the lane's own 16 scores: m_run is the same on the row's 4 lanes, so "some lane grew" is "the
-      // row grew"; the cross-lane row max is only formed when the wave rescales
-      mx[qi] = m;
-      grow |= m > m_run[qi] + thr;
+      mx[qi] = rowmax4_asm(m);
+      grow |= mx[qi] > m_run[qi] + thr;
     }
     if (__any(grow)) {  // wave-uniform; every tile while m_run = -inf, rarely afterwards
 #pragma unroll
       for (int qi = 0; qi < QI; ++qi) {
-        const float m_new = fmaxf(m_run[qi], rowmax4_asm(mx[qi]));
+        const float m_new = fmaxf(m_run[qi], mx[qi]);
         const float alpha = fast_exp2((m_run[qi] - m_new) * c2);  // first tile: exp2(-inf) = 0
         lsum[qi] *= alpha;
 #pragma unroll

@@ -230,6 +230,7 @@ def test_graph_epoch_equals_eager_epoch(cuda):
 
     u_e, tr_e = make()
     u_g, tr_g = make()
+    u_e2, tr_e2 = make()  # a second eager run: the run-to-run spread of the float-atomic dW sums, for the bars below
     g = torch.Generator(device="cuda").manual_seed(5)
     Bp = P * gas
     enc = torch.randn(Bp, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
@@ -241,23 +242,32 @@ def test_graph_epoch_equals_eager_epoch(cuda):
         sb = tr_e.shuffle(buf, generator=torch.Generator(device="cuda").manual_seed(100 + epoch))
         tr_e.train_epoch(sb)
         tr_g.train_epoch_graph(sb)
+        tr_e2.train_epoch(sb)
     torch.cuda.synchronize()
     assert tr_g._graph is not None and tr_g.opt_step == tr_e.opt_step == 3
     le = torch.stack(tr_e.loss_hist).cpu()
     lg = torch.stack(tr_g.loss_hist).cpu()
+    le2 = torch.stack(tr_e2.loss_hist).cpu()
     # epoch 0 runs before any update: same kernels on the same inputs -> same loss.  Later epochs start from LoRA
-    # weights that differ by the float-atomic rounding of the dW kernels (<= 1e-5 below), which beta = 50 amplifies
-    # in the loss (measured up to 5e-3 rel on the third epoch)
+    # weights that differ by the float-atomic rounding of the dW kernels, which beta = 50 and this test's large lr
+    # (the loss falls 0.6 -> 0.08 in two updates) amplify; the graph replay must stay within that run-to-run spread
+    # (measured by the second eager run: 3x its spread, floor 2 % rel)
     assert torch.allclose(le[0], lg[0], rtol=1e-5, atol=1e-6), (le, lg)
-    assert torch.allclose(le, lg, rtol=2e-2, atol=1e-4), (le, lg)
+    spread = (le - le2).abs()
+    bar = torch.maximum(3 * spread, 2e-2 * le.abs()) + 1e-4
+    assert ((le - lg).abs() <= bar).all(), (le, lg, le2)
+    print(f"graph-vs-eager losses {lg.tolist()} vs {le.tolist()}, eager-vs-eager spread {spread.tolist()}")
     # the LoRA dW kernels accumulate with float atomics, so grads agree to rounding, not bitwise; AdamW turns a
-    # rounding difference on a near-zero gradient into up to ~lr of parameter change: bar 1 % of lr = 1e-5
-    assert torch.allclose(u_e.lora.master, u_g.lora.master, rtol=0, atol=1e-5), \
-        (u_e.lora.master - u_g.lora.master).abs().max().item()
+    # rounding difference on a near-zero gradient into up to ~lr of parameter change: bar 1 % of lr = 1e-5, or 3x the
+    # eager run-to-run spread
+    wbar = max(1e-5, 3 * (u_e.lora.master - u_e2.lora.master).abs().max().item())
+    assert (u_e.lora.master - u_g.lora.master).abs().max().item() <= wbar, \
+        ((u_e.lora.master - u_g.lora.master).abs().max().item(), wbar)
     # moments: the float-atomic dW sums differ in their last bits between the two runs, and where an element's sum
     # cancels that difference is large RELATIVE to the element; bar it against the tensor's scale instead
-    for a, b in ((tr_e.exp_avg, tr_g.exp_avg), (tr_e.exp_avg_sq, tr_g.exp_avg_sq)):
-        assert (a - b).abs().max().item() <= 1e-4 * a.abs().max().item() + 1e-12, (a - b).abs().max().item()
+    for a, b, c in ((tr_e.exp_avg, tr_g.exp_avg, tr_e2.exp_avg), (tr_e.exp_avg_sq, tr_g.exp_avg_sq, tr_e2.exp_avg_sq)):
+        mbar = max(1e-4 * a.abs().max().item(), 3 * (a - c).abs().max().item()) + 1e-12
+        assert (a - b).abs().max().item() <= mbar, ((a - b).abs().max().item(), mbar)
 
 
 def test_full_unet_micro_step_vs_fp32_reference(cuda):
