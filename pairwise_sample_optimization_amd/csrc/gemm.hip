@@ -19,6 +19,8 @@
 // holding 4 consecutive output columns of one row -> 8-B / 16-B vector epilogue stores.
 #include "common.h"
 
+#include <cstdlib>
+
 #define GEMM_THREADS 256
 #define BK 64
 
@@ -899,6 +901,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
 // Split-K over gridDim.y with f32 atomics in the epilogue (output is always an f32 accumulator).
 // =====================================================================================================================
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_g;
+typedef __attribute__((address_space(3))) void tnr_lds_void_g;
 __device__ __forceinline__ int swz_tr64(int r, int c) { return r * 64 + ((c ^ (((r >> 1) & 3) << 1)) << 3); }
 
 __device__ __forceinline__ s16x4 tr_read64(const bf16_t* img, int r0, int col0, int lane) {
@@ -1000,6 +1003,122 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int M, int I, int J, co
           if (gridDim.y > 1) atomicAdd(o, acc[a][b][r] * alpha);
           else *o += acc[a][b][r] * alpha;
         }
+    }
+  }
+}
+
+// 128 x 128 TN tile for the full-weight gradients (C3 / C4: dW = X^T dY over the B*H*W tokens, I, J >= 128):
+// 4 waves of 64 x 64 (4 x 4 MFMA tiles, every operand fragment feeds four MFMAs), 64-token K-steps staged by
+// buffer_load ... lds (each wave one 64 x 64 image: A cols i0.. / i0+64.., B cols j0.. / j0+64..; source-side
+// swizzle for the transposed reads; rows past M read as zeros) through a 2-stage ring, fragments by inline-asm
+// ds_read_b64_tr_b16 (the builtin makes hipcc drain the LDS-DMA ring).  Split-K over gridDim.y with f32 atomics.
+__device__ __forceinline__ s16x4 tn_tr_asm(unsigned img_base, int r0, int col0, int lane) {
+  const int li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+  const int col = col0 + 4 * p;
+  const unsigned addr = img_base + 2u * (unsigned)(swz_tr64(r0 + q, col >> 3) + (col & 7));
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J, const bf16_t* __restrict__ A,
+                                                            long lda, const bf16_t* __restrict__ B, long ldb,
+                                                            float alpha, float* __restrict__ out, long ldo,
+                                                            int steps) {
+  __shared__ __attribute__((aligned(16))) bf16_t sT[2][4][64 * 64];  // [stage][A0 A1 B0 B1], 64 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
+  const int g = lane >> 4, c = lane & 15;
+  const int nbj = (J + 127) / 128;
+  const int bi = blockIdx.x / nbj, bj = blockIdx.x - bi * nbj;
+  const int i0 = bi * 128, j0 = bj * 128;
+  const int nkt = (M + 63) / 64;
+  const int t_beg = blockIdx.y * steps, t_end = min(nkt, t_beg + steps);
+  // wave w stages image w: A (w < 2) or B, 64 columns from col0, all 8 pieces of 8 rows x 128 B
+  const bool isA = wave < 2;
+  const long ld = isA ? lda : ldb;
+  const int col0 = (isA ? i0 : j0) + (wave & 1) * 64;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(isA ? A : B), (short)0, (int)(((long)(M - 1) * ld + (isA ? I : J)) * 2), 0x00020000);
+  const int prow = lane >> 3, pch = lane & 7;
+  const int sc = pch ^ (((prow >> 1) & 3) << 1);  // source chunk landing at LDS chunk pch (swz_tr64)
+  // columns past I / J are clamped to the last 8 (their products land in unstored outputs)
+  const int cw = min(col0 + sc * 8, (isA ? I : J) - 8);
+  const unsigned voff = (unsigned)((long)prow * ld + cw) * 2u;
+  const int kstep = (int)(64 * ld * 2);
+  auto issue = [&](int t, int stg) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (tnr_lds_void_g*)(sT[stg][wave] + p * 8 * 64), 16,
+                                               voff + (unsigned)(p * 8 * ld * 2), t * kstep, 0, 0);
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned lbase = (unsigned)(uintptr_t)(const tnr_lds_void_g*)&sT[0][0][0];
+  if (t_beg < t_end) issue(t_beg, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int t = t_beg; t < t_end; ++t) {
+    const int cur = (t - t_beg) & 1;
+    if (t + 1 < t_end) issue(t + 1, cur ^ 1);
+    const unsigned ia = lbase + (unsigned)((cur * 4 + wi) * 64 * 64 * 2);
+    const unsigned ib = lbase + (unsigned)((cur * 4 + 2 + wj) * 64 * 64 * 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s16x4 ra[8], rb[8];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        ra[2 * a] = tn_tr_asm(ia, ks * 32 + 8 * g, a * 16, lane);
+        ra[2 * a + 1] = tn_tr_asm(ia, ks * 32 + 8 * g + 4, a * 16, lane);
+        rb[2 * a] = tn_tr_asm(ib, ks * 32 + 8 * g, a * 16, lane);
+        rb[2 * a + 1] = tn_tr_asm(ib, ks * 32 + 8 * g + 4, a * 16, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(ra[0]), "+v"(ra[1]), "+v"(ra[2]), "+v"(ra[3]), "+v"(ra[4]), "+v"(ra[5]), "+v"(ra[6]),
+                     "+v"(ra[7]), "+v"(rb[0]), "+v"(rb[1]), "+v"(rb[2]), "+v"(rb[3]), "+v"(rb[4]), "+v"(rb[5]),
+                     "+v"(rb[6]), "+v"(rb[7]));
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x8 va = {ra[2 * a][0], ra[2 * a][1], ra[2 * a][2], ra[2 * a][3],
+                    ra[2 * a + 1][0], ra[2 * a + 1][1], ra[2 * a + 1][2], ra[2 * a + 1][3]};
+        s16x8 vb = {rb[2 * a][0], rb[2 * a][1], rb[2 * a][2], rb[2 * a][3],
+                    rb[2 * a + 1][0], rb[2 * a + 1][1], rb[2 * a + 1][2], rb[2 * a + 1][3]};
+        af[a] = __builtin_bit_cast(bf16x8, va);
+        bfr[a] = __builtin_bit_cast(bf16x8, vb);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // the next stage landed (every wave's pieces), and every wave's reads of this stage retired before it is restaged
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // lane holds out[i = i0 + wi*64 + a*16 + c][j = j0 + wj*64 + b*16 + 4g + r]
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = i0 + wi * 64 + a * 16 + c;
+    if (i >= I) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + wj * 64 + b * 16 + 4 * g;
+      if (j >= J) continue;  // J % 8 == 0: a lane's 4 columns are all in or all out
+      float* o = out + (long)i * ldo + j;
+      if (gridDim.y > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(o + r, acc[a][b][r] * alpha);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] += acc[a][b][r] * alpha;
+      }
     }
   }
 }
@@ -1183,8 +1302,33 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
       return pso_gemm_tn_rank(M, J, B, ldb, A, lda, I, 0, alpha, out, ldo, 1, (hipStream_t)stream);
   }
   PSO_ARG_CHECK(group == 0, "pso_gemm_tn: grouped form needs a rank-32/64/96 side and 128 | group");
-  const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
   const int nkt = (M + 63) / 64;
+  // full-weight gradients (both sides >= 128 wide): 128 x 128 tiles; split over M only as far as needed to cover ~2
+  // rounds of co-resident blocks (each split adds its tile of f32 atomics)
+  static const int tn128 = [] {
+    const char* e = getenv("PSO_TN128");  // benchmark knob: 0 keeps the 64 x 64 kernel everywhere
+    return e ? atoi(e) : 1;
+  }();
+  const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
+  if (tn128 && g_tn_split == 0 && I >= 128 && J >= 128 && (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30)) {
+    // split over M only while its f32 atomics stay small next to the product: each split adds I*J*4 bytes at the
+    // ~1.3 TB/s atomic rate against 2*M*I*J flop, so ks <= M / 16384 keeps them under ~10 %
+    int ks = (512 + t128 - 1) / t128;
+    if (ks > M / 16384) ks = M / 16384;
+    if (ks < 1) ks = 1;
+    const int steps = (nkt + ks - 1) / ks;
+    ks = (nkt + steps - 1) / steps;
+  // fewer than 128 blocks (e.g. 640 x 640 weights: 25 tiles) leave most CUs idle: the 64 x 64 kernel's 4x the tiles
+  // win there (C3 step shape_prof: 24576 x 640 x 640 122 vs 59 TF/s, 6144 x 1280 x 1280 234 vs 213; the 128 x 128
+  // tiles elsewhere: 6144 x 10240 x 1280 697 vs 417, 98304 x 320 x 2880 485 vs 141, 6144 x 1280 x 11520 815 vs 431)
+  if (t128 * ks >= 128) {
+    pso_note_kernel("gemm_tn128_kernel");
+    gemm_tn128_kernel<<<dim3(t128, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda,
+                                                                        (const bf16_t*)B, ldb, alpha, out, ldo, steps);
+    return pso_check_launch("pso_gemm_tn");
+  }
+  }
+  const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
   // ~160 blocks: fewer leaves the M-range latency-bound, more multiplies the f32 atomics (measured optimum on the
   // LoRA dW shapes, M = 4096 / 16384, I x J = 1280x32 .. 640x32)
   int ks = g_tn_split > 0 ? g_tn_split : (160 + tiles - 1) / tiles;

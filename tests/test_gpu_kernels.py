@@ -132,7 +132,10 @@ def test_conv_stride1_input_grad_flipped(cuda):
 
 @pytest.mark.parametrize("M,I,J", [(16384, 96, 640), (308, 32, 2048), (4096, 1280, 32), (100, 64, 8),
                                    (8192, 1280, 32), (8192, 32, 1280), (8192, 96, 1280), (616, 64, 2048),
-                                   (1000, 640, 64), (616, 1280, 32), (77, 32, 256)])
+                                   (1000, 640, 64), (616, 1280, 32), (77, 32, 256),
+                                   # full-weight gradients (128 x 128 TN tiles): ragged M / I / J, split-K atomics
+                                   (16384, 1280, 1280), (1000, 640, 320), (616, 2880, 640), (77, 136, 264),
+                                   (16384, 128, 128), (4100, 1152, 320)])
 def test_gemm_tn_vs_fp32(cuda, M, I, J):
     """Generic TN path and the streaming rank-r path (one side 32 / 64 / 96 wide), partial 64-row steps included."""
     from pairwise_sample_optimization_amd import kernels as K_
