@@ -6,7 +6,18 @@ sampler (T = 1 trained transition; a literal 1-step sampler trains nothing, SURV
 optimizer step = gas*T micro-steps (+ the per-inner-epoch buffer shuffle, RCCL all-reduce, clip, AdamW); each
 micro-step trains 2P images (2P policy UNet fwd+bwd + 2P reference fwd + fused loss).  Synthetic data: random-init
 SDXL weights (seeded), N(0,1) text embeddings, trajectories from this build's own sampler (untimed), U(0,1)
-rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling), RCCL all-reduce of the flat LoRA grads.
+rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling); the LoRA gradient is all-reduced over RCCL in
+~32 MB buckets issued during the backward of the window's last micro-step (GradBuckets), overlapped with it.
+
+Secondary objects on the same JSON line (never the headline value):
+  "c3"        BASELINE configs[2] on this GPU: SDXL-DMD2 PSO, 4-step sampler (T = 3), full-UNet grads against a frozen
+              reference UNet, 1 pair per micro-step -- its own warmed-up, timed steps + dominant-kernel roofline;
+  "lora_bs1"  the north-star operating point "bs = 1 / GPU": the C2 LoRA step at 1 pair, gas 1 (one micro-step =
+              2 policy + 2 reference images in one paired pass);
+  "dist"      (N > 1) the backend and world size torch.distributed really runs, every rank's ms/step, and the
+              bucketed all-reduce: bytes on the wire, its time alone, and the part of it left exposed after the
+              backward (the rest ran under the backward).
+  Both config objects run at N = 1 only (--no-extra skips them).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   Under torchrun (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one rank.  Started directly with --gpus N > 1,
@@ -54,6 +65,10 @@ def parse():
     ap.add_argument("--full-unet", action="store_true",
                     help="train every UNet parameter against a frozen reference UNet (BASELINE C3 / C4; use with "
                          "--mode dmd --num-steps 4 --pairs 1 --gas 1)")
+    ap.add_argument("--allreduce-bf16", action="store_true",
+                    help="bf16 gradient all-reduce (fp32 accumulation and optimizer; half the xGMI bytes)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c3 / lora_bs1 secondary objects")
+    ap.add_argument("--extra-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -82,7 +97,8 @@ def build(args, dev):
         unet.lora.init_gaussian(seed=0, b_std=1e-3)  # non-zero B so policy != reference
     unet.prepare()
     tr = PSOTrainer(unet, mode=args.mode, num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
-                    train_batch_size=args.pairs, num_reward=1, ref_unet=ref_unet)
+                    train_batch_size=args.pairs, num_reward=1, ref_unet=ref_unet,
+                    allreduce_dtype=torch.bfloat16 if getattr(args, "allreduce_bf16", False) else None)
     g = torch.Generator(device=dev).manual_seed(1000 + int(os.environ.get("RANK", "0")))
     Bp = args.pairs * args.gas  # pairs sampled per epoch per GPU
     enc = torch.randn(Bp, 77, 2048, device=dev, generator=g).bfloat16()
@@ -184,6 +200,7 @@ def cpu_baseline(args, unet):
 
 
 SDXL_FWD_TFLOP_PER_IMG = 6.765   # one UNet forward at 1024^2
+SURVEY_TFLOP_FULL_UNET = 54.10   # one pair-micro-step with full-UNet grads at 1024^2
 VAE_DEC_TFLOP_PER_IMG = 10.49    # AutoencoderKL.decode at 1024^2
 
 
@@ -235,6 +252,66 @@ def epoch_metric(args, dev, tr, buf, g, n_epochs):
         out["tflop_per_epoch_per_gpu"] = round(tf, 1)
         out["mfma_frac"] = round(tf / dt / PEAK_BF16_TFLOPS, 4)
     del vae, sel
+    return out
+
+
+def sub_config(args, dev, name, steps, warmup=1, **over):
+    """One secondary configuration on this GPU (a fresh model / trainer / buffer; the headline's objects must be freed
+    by the caller first): warmup, `steps` timed train steps, its dominant-kernel roofline."""
+    import copy
+    a = copy.copy(args)
+    for k, v in over.items():
+        setattr(a, k, v)
+    unet, tr, buf, g = build(a, dev)
+    for _ in range(warmup):
+        one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step(tr, buf, g)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    imgs = 2 * a.pairs * a.gas * (a.num_steps - 1)
+    out = {"imgs_per_s": round(imgs / dt, 3), "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": warmup,
+           "imgs_per_step": imgs, "loss": round(torch.stack(tr.loss_hist[-2:]).mean().item(), 6)}
+    pair_micro = a.pairs * a.gas * (a.num_steps - 1)
+    tf = SURVEY_TFLOP_FULL_UNET if a.full_unet else SURVEY_TFLOP_PER_PAIR_MICRO.get(a.rank)
+    if a.res == 1024 and tf:
+        out["tflop_per_step"] = round(tf * pair_micro, 2)
+        out["step_mfma_frac"] = round(tf * pair_micro / dt / PEAK_BF16_TFLOPS, 4)
+    if not a.no_roofline:
+        rf = roofline(tr, buf, g)
+        out["roofline"] = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "avg_launch_us",
+                                              "launches_per_step", "share_of_family_time", "family")}
+    del unet, tr, buf
+    torch.cuda.empty_cache()
+    log(f"[bench] {name}: {out['imgs_per_s']} imgs/s ({out['ms_per_step']} ms/step)")
+    return out
+
+
+def dist_report(tr, dev, dt_rank, steps):
+    """What torch.distributed really ran (backend, world) and the overlap of the gradient all-reduce with the
+    backward: exposed = the compute stream's wait for RCCL after the window's last backward (GradBuckets.finish,
+    HIP events on the compute stream); alone = the same buckets all-reduced with nothing beside them."""
+    world = dist.get_world_size()
+    per = torch.tensor([dt_rank / steps * 1e3], dtype=torch.float64, device=dev)
+    allp = [torch.zeros_like(per) for _ in range(world)]
+    dist.all_gather(allp, per)
+    out = {"backend": dist.get_backend(), "world_size": world,
+           "rank_ms_per_step": [round(t.item(), 2) for t in allp]}
+    gb = tr.buckets
+    if gb is not None:
+        exp = [a.elapsed_time(b) for a, b in gb.exposed_ms]
+        gb.exposed_ms = []
+        alone = gb.alone_ms()
+        from pairwise_sample_optimization_amd import kernels as K
+        K.zero_(gb.flat)
+        out["allreduce"] = {"buckets": len(gb.buckets), "bytes_on_wire": gb.bytes_on_wire(),
+                            "wire_dtype": str(gb.wire_dtype or gb.flat.dtype).replace("torch.", ""),
+                            "alone_ms": round(alone, 3) if alone is not None else None,
+                            "exposed_ms_per_step": round(sum(exp) / max(len(exp), 1), 3) if exp else None}
+        if exp and alone:
+            out["allreduce"]["hidden_frac"] = round(max(0.0, 1.0 - (sum(exp) / len(exp)) / alone), 3)
     return out
 
 
@@ -290,6 +367,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if tr.buckets is not None:
+        tr.buckets.timing = True
+        tr.buckets.exposed_ms = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_step(tr, buf, g, graph=args.graph)
@@ -297,8 +377,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, dev)
+    dt_rank = time.perf_counter() - t0
+    dt = max_over_ranks(dt_rank, dev)
+    if tr.buckets is not None:
+        tr.buckets.timing = False
     imgs_per_step_gpu = 2 * args.pairs * args.gas * (args.num_steps - 1)
     value = imgs_per_step_gpu * world * args.steps / dt
     ms = dt / args.steps * 1e3
@@ -323,6 +405,8 @@ def main():
     if tf:
         step_tf = tf * args.pairs * args.gas * (args.num_steps - 1)
         res["step_mfma_frac"] = round(step_tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)
+    if world > 1:
+        res["dist"] = dist_report(tr, dev, dt_rank, args.steps)
     if not args.no_roofline:
         res["roofline"] = roofline(tr, buf, g)
     if args.epochs > 0:
@@ -331,6 +415,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline ...")
         res["cpu_baseline"] = cpu_baseline(args, unet)
+    if world == 1 and not args.no_extra and not args.full_unet and args.res == 1024:
+        del unet, tr, buf
+        torch.cuda.empty_cache()
+        log("[bench] lora_bs1 ...")
+        res["lora_bs1"] = dict(sub_config(args, dev, "lora_bs1", args.extra_steps + 2, warmup=2, pairs=1, gas=1),
+                               workload="C2 LoRA r=%d step at 1 pair / GPU, gas 1: 2 policy + 2 reference images per "
+                                        "paired pass (north-star bs=1/GPU)" % args.rank)
+        log("[bench] c3 ...")
+        res["c3"] = dict(sub_config(args, dev, "c3", args.extra_steps, warmup=1, mode="dmd", num_steps=4, pairs=1,
+                                    gas=1, full_unet=True),
+                         workload="C3: SDXL-DMD2 PSO, 4-step sampler (T=3), full-UNet grads vs a frozen reference UNet, "
+                                  "1 pair / micro-step, gas 1, bf16, 1024^2")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -347,7 +347,10 @@ __device__ __forceinline__ s16x4 tr_read_imm(unsigned base) {
   return v;
 }
 
-template <int QI>
+// LG (lane-local growth test, the round-2 variant ea590ae): the rescale test runs on each lane's own 16 scores (m_run
+// is the same on a row's 4 lanes, so "some lane grew" == "the row grew") and the cross-lane row max is formed only
+// inside the (rare) rescale branch.  Same decisions, same arithmetic: outputs bit-identical to LG = false.
+template <int QI, bool LG = false>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, int nqb) {
   constexpr int STG = 3;
   constexpr int PIECES = 4;
@@ -481,13 +484,13 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, i
       m = vmax3(m, s[qi][2][3], s[qi][3][0]);
       m = vmax3(m, s[qi][3][1], s[qi][3][2]);
       m = vmax2(m, s[qi][3][3]);
-      mx[qi] = rowmax4_asm(m);
+      mx[qi] = LG ? m : rowmax4_asm(m);
       grow |= mx[qi] > m_run[qi] + thr;
     }
     if (__any(grow)) {  // wave-uniform; every tile while m_run = -inf, rarely afterwards
 #pragma unroll
       for (int qi = 0; qi < QI; ++qi) {
-        const float m_new = fmaxf(m_run[qi], mx[qi]);
+        const float m_new = fmaxf(m_run[qi], LG ? rowmax4_asm(mx[qi]) : mx[qi]);
         const float alpha = fast_exp2((m_run[qi] - m_new) * c2);  // first tile: exp2(-inf) = 0
         lsum[qi] *= alpha;
 #pragma unroll
@@ -1006,10 +1009,11 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // workgroups, else 128 (4 x 32): fewer K/V LDS bytes per MFMA vs. a fuller grid
   const int nq4 = cdiv(Sq, 256), nq2 = cdiv(Sq, 128);
   // cross-attention (77 keys: two key tiles) keeps 128: its per-workgroup set-up outweighs the K/V reuse (-10 %)
-  // fwd variant knob (benchmarks only): 0 auto, 2 / 4 force 32 / 64 rows per wave, +5 (5, 7, 9) the first-round loop
+  // fwd variant knob (benchmarks / tests): 0 auto, 1 auto with the lane-local growth test (LG), 2 / 4 force 32 / 64
+  // rows per wave, +5 (5, 7, 9) the first-round loop
   const int fv = g_attn_fwd_variant;
   const int qsel = fv >= 5 ? fv - 5 : fv;
-  const bool big = qsel == 4 || (qsel == 0 && (long)nq4 * H * B >= 1024 && Sk > 128);
+  const bool big = qsel == 4 || ((qsel == 0 || qsel == 1) && (long)nq4 * H * B >= 1024 && Sk > 128);
   hipStream_t st = (hipStream_t)stream;
   if (g_attn_vsum) {
     if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
@@ -1017,6 +1021,9 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   } else if (fv >= 5) {
     if (big) attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
     else attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
+  } else if (fv == 1) {  // lane-local growth test (LG)
+    if (big) attn_fwd2_kernel<4, true><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
+    else attn_fwd2_kernel<2, true><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
   } else if (big) {
     attn_fwd2_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
   } else {

@@ -57,16 +57,22 @@ def shuffle_index(perm, perms, P):
     return img_idx, pair_img, tsel_i
 
 
-def allreduce_grads(flat, process_group=None):
-    """DDP gradient sync of the flat LoRA grad bucket (T:857 under accelerate: all-reduce SUM, then the mean).  The
-    1/world factor is returned, not applied: the clip and AdamW kernels fold it into their gradient read, so the
-    bucket is touched once by RCCL and once by the optimizer."""
+def allreduce_grads(flat, process_group=None, wire_dtype=None):
+    """DDP gradient sync of the flat trained gradient in one collective (T:857 under accelerate: all-reduce SUM, then
+    the mean) -- the path when no overlapped GradBuckets sync was armed (hipGraph epochs).  The 1/world factor is
+    returned, not applied: the clip and AdamW kernels fold it into their gradient read.  wire_dtype=torch.bfloat16
+    reduces a bf16 copy and casts the sum back (half the bytes; fp32 accumulation stays local)."""
     if not (dist.is_available() and dist.is_initialized()):
         return 1.0
     world = dist.get_world_size(process_group)
     if world == 1:
         return 1.0
-    dist.all_reduce(flat, group=process_group)
+    if wire_dtype is not None and wire_dtype != flat.dtype:
+        t = flat.to(wire_dtype)
+        dist.all_reduce(t, group=process_group)
+        flat.copy_(t)
+    else:
+        dist.all_reduce(flat, group=process_group)
     return 1.0 / world
 
 
@@ -79,10 +85,17 @@ class GradBuckets:
     far, beside the rest of the backward.  finish() issues whatever is left and makes the compute stream wait for
     every bucket before the clip / AdamW read the gradient.  The 1/world mean is folded into those kernels."""
 
-    def __init__(self, unet, flat, bucket_mb=32.0, process_group=None):
+    def __init__(self, unet, flat, bucket_mb=32.0, process_group=None, wire_dtype=None):
         self.flat = flat
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        # wire_dtype=torch.bfloat16: every bucket is cast to bf16 for the all-reduce and cast back into the fp32 flat
+        # gradient afterwards (what DDP's bf16_compress_hook does): half the xGMI bytes -- 5.1 instead of 10.3 GB per
+        # full-UNet step (C4) -- while the local accumulation over the window's micro-steps stays fp32
+        self.wire_dtype = wire_dtype
+        self.timing = False      # record the compute-stream stall on the outstanding buckets (bench diagnostics)
+        self.exposed_ms = []     # per finish(): ms the compute stream waited for RCCL after the backward
+        self._ev = None
         cap = int(bucket_mb * 1e6 / flat.element_size())
         self.buckets = []        # [(offset, numel, last unit)]
         self.unit_bucket = {}    # unit -> bucket index (every unit of the bucket)
@@ -111,6 +124,7 @@ class GradBuckets:
     def reset(self):
         self.pending = [set(u) for _, _, u in self.buckets]
         self.works = [None] * len(self.buckets)
+        self.wire = [None] * len(self.buckets)
 
     def _issue(self, b, side=None):
         if self.works[b] is not None:
@@ -118,7 +132,15 @@ class GradBuckets:
         if side is not None:
             side.join()  # LoRA dW launches on the side stream belong to this bucket
         off, n, _ = self.buckets[b]
-        self.works[b] = dist.all_reduce(self.flat[off:off + n], group=self.pg, async_op=True)
+        t = self.flat[off:off + n]
+        if self.wire_dtype is not None and self.wire_dtype != t.dtype:
+            t = t.to(self.wire_dtype)  # cast on the compute stream; the collective is ordered after it
+            self.wire[b] = t
+        self.works[b] = dist.all_reduce(t, group=self.pg, async_op=True)
+
+    def bytes_on_wire(self):
+        es = torch.empty((), dtype=self.wire_dtype or self.flat.dtype).element_size()
+        return sum(n for _, n, _ in self.buckets) * es
 
     def hook(self, rt):
         """rt.unit_done for one backward pass (the pass that ends an accumulation window)."""
@@ -134,13 +156,51 @@ class GradBuckets:
         return unit_done
 
     def finish(self):
-        """Issue the buckets not reported (none on the normal path), then wait for all of them; returns 1/world."""
+        """Issue the buckets not reported (none on the normal path), then wait for all of them; returns 1/world.
+        With RCCL the waits are stream waits: the compute stream (clip / AdamW next) queues behind each bucket's
+        collective, the host does not block.  bf16 wire buckets are cast back into the fp32 gradient here."""
         for b in range(len(self.buckets)):
             self._issue(b)
-        for w in self.works:
+        if self.timing and torch.cuda.is_available() and self.flat.is_cuda:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        else:
+            e0 = None
+        for b, w in enumerate(self.works):
             w.wait()
+            if self.wire[b] is not None:
+                off, n, _ = self.buckets[b]
+                self.flat[off:off + n].copy_(self.wire[b])
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.exposed_ms.append((e0, e1))
         self.reset()
         return 1.0 / self.world
+
+    def alone_ms(self, reps=3):
+        """Time the window's all-reduces with nothing beside them (every bucket issued back to back, then waited):
+        the denominator of the hidden-under-backward fraction.  Sums into the gradient: callers zero it after."""
+        dev_ev = self.flat.is_cuda
+        times = []
+        for _ in range(reps):
+            if dev_ev:
+                torch.cuda.synchronize()
+            dist.barrier(group=self.pg)
+            t0 = torch.cuda.Event(enable_timing=True) if dev_ev else None
+            if dev_ev:
+                t0.record()
+            for b in range(len(self.buckets)):
+                self._issue(b)
+            for b, w in enumerate(self.works):
+                w.wait()
+            if dev_ev:
+                t1 = torch.cuda.Event(enable_timing=True)
+                t1.record()
+                torch.cuda.synchronize()
+                times.append(t0.elapsed_time(t1))
+            self.reset()
+        return min(times) if times else None
 
 
 def trainable(unet):
@@ -163,7 +223,7 @@ def lora_optimizer_step(tr):
         scale = tr.buckets.finish()
         tr.sync_armed = False
     else:
-        scale = allreduce_grads(grad, tr.pg)
+        scale = allreduce_grads(grad, tr.pg, getattr(tr, "allreduce_dtype", None))
     K.grad_clip_coef(grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
     tr.opt_step += 1
     K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
@@ -176,7 +236,7 @@ class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
                  train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None,
-                 latent_dtype=torch.float32):
+                 latent_dtype=torch.float32, allreduce_dtype=None):
         self.unet = unet
         if mode not in ("turbo", "dmd"):
             raise ValueError(f"mode must be 'turbo' or 'dmd', got {mode!r}")
@@ -209,8 +269,10 @@ class PSOTrainer:
         self.loss_hist = []
         # overlapped bucketed all-reduce on multi-GPU runs (GradBuckets); off inside hipGraph capture
         self.overlap_sync = self.world > 1
-        self.buckets = GradBuckets(unet, trainable(unet)[1], process_group=process_group) if self.overlap_sync \
-            else None
+        self.allreduce_dtype = allreduce_dtype
+        # allreduce_dtype=torch.bfloat16: bf16 on the wire, fp32 accumulation and optimizer (GradBuckets)
+        self.buckets = GradBuckets(unet, trainable(unet)[1], process_group=process_group,
+                                   wire_dtype=allreduce_dtype) if self.overlap_sync else None
         self.sync_armed = False
         self.max_pass_images = max_pass_images  # images per batched UNet pass (HBM budget: ~5 GB saved each @1024^2)
         self.auto_step = True  # run the optimizer every gas*T micro-steps (tests may inspect raw grads)
@@ -230,15 +292,28 @@ class PSOTrainer:
 
     @classmethod
     def from_config(cls, unet, config, mode="turbo", num_reward=1, process_group=None, ref_unet=None,
-                    latent_dtype=torch.float32):
+                    latent_dtype=None):
         """Build from a reference run config (`config_sdxl_{turbo,dmd}_dpo.get_config()`): sample.num_steps,
         train.{beta, eps, learning_rate, adam_*, max_grad_norm, gradient_accumulation_steps, batch_size}.
         Both trainers require `distilled_train_steps == num_steps - 1` (turbo asserts it at T:221; DMD2 asserts
-        `<=` at D:225 and the trajectory length `==` at D:719-720)."""
+        `<=` at D:225 and the trajectory length `==` at D:719-720).
+        latent_dtype (DMD2 only): None follows `config.mixed_precision` as the reference does -- its latents are
+        weight_dtype (D:329-333; drawn in prompt_embeds.dtype, DP/sdxl_dmd_with_logprob.py:91-101), so its step /
+        log-prob arithmetic runs in that dtype (DP/distilled_inference_with_logprob.py:84-135) -> the replay mode of
+        that dtype; pass torch.float32 to train on the fp32 step math instead.  A value that disagrees with the
+        config is honoured with a warning."""
         tr = config.train
         if tr.distilled_train_steps != config.sample.num_steps - 1:
             raise AssertionError("train.distilled_train_steps must equal sample.num_steps - 1 "
                                  f"({tr.distilled_train_steps} vs {config.sample.num_steps - 1})")
+        mp = getattr(config, "mixed_precision", "no")
+        cfg_dtype = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(mp, torch.float32)
+        if latent_dtype is None:
+            latent_dtype = cfg_dtype if mode == "dmd" else torch.float32
+        elif mode == "dmd" and latent_dtype != cfg_dtype:
+            import warnings
+            warnings.warn(f"PSOTrainer.from_config: latent_dtype {latent_dtype} differs from the config's "
+                          f"mixed_precision={mp!r} (reference latents: {cfg_dtype})")
         return cls(unet, mode=mode, num_steps=config.sample.num_steps, beta=float(tr.beta), clip_eps=float(tr.eps),
                    lr=tr.learning_rate, betas=(tr.adam_beta1, tr.adam_beta2), weight_decay=tr.adam_weight_decay,
                    adam_eps=tr.adam_epsilon, max_grad_norm=tr.max_grad_norm,
@@ -439,7 +514,9 @@ class PSOTrainer:
         g = getattr(self, "_graph", None)
         if g is None or self._graph_key != key:
             self._graph = None
-            self.overlap_sync = False  # no collective inside the captured region: the step's all-reduce is eager
+            # no collective inside the captured region: the step's all-reduce is eager.  Only the warm-up and the
+            # capture run without the overlapped bucketed sync; eager epochs afterwards get it back (finally below).
+            overlap0, self.overlap_sync = self.overlap_sync, False
             self._gsb = SimpleNamespace(n_micro=sb.n_micro, P=sb.P,
                                         **{k: getattr(sb, k).clone() for k in self._SB_TENSORS})
             _, st_grad, _ = trainable(self.unet)
@@ -456,6 +533,7 @@ class PSOTrainer:
                 self._gloss = self.loss_hist[h1:]
             finally:
                 self.auto_step = True
+                self.overlap_sync = overlap0
                 self.n_micro = n0
                 del self.loss_hist[h0:]
                 st_grad.copy_(saved)

@@ -1099,11 +1099,23 @@ class UNet2DConditionModel(nn.Module):
         return self
 
     def _fp8_weight(self, key, w, version=0):
-        """(e4m3 [N, K], E8M0 [N]) of a weight, quantised per output channel once per (key, version)."""
+        """(e4m3 [N, K], E8M0 [N]) of a weight, quantised per output channel.  Frozen base weights (version 0) are
+        quantised once and cached.  The LoRA sB stacks (version > 0) change at every optimizer step: they are
+        re-quantised on EVERY forward into buffers allocated once, so a hipGraph capture of the epoch records the
+        quantisation kernel and each replay reads the current LoRA weights (a version-keyed cache hit would record
+        nothing and replay the capture-time copies).  The sB stacks are [C, r]-sized: the extra pass is negligible."""
         hit = self._fp8_cache.get(key)
-        if hit is None or hit[0] != version:
+        if version == 0:
+            if hit is None:
+                hit = (0, K.quant_rows_fp8(w))
+                self._fp8_cache[key] = hit
+            return hit[1]
+        if hit is None or hit[1][0].shape != w.shape:
             hit = (version, K.quant_rows_fp8(w))
             self._fp8_cache[key] = hit
+            return hit[1]
+        q, e = hit[1]
+        K.quant_rows_fp8(w, q=q, e=e)
         return hit[1]
 
     def kv_text(self, rt, C):

@@ -234,10 +234,15 @@ class AutoencoderKL(nn.Module):
         return self._decode_padded(zp)
 
     def _decode_padded(self, zp):
-        """Images in chunks whose largest activation ([n, 8h, 8w, 256] at the last upsampler) stays under 2^30
-        elements: the kernels' per-operand 32-bit element offsets (4 images per chunk at 1024^2)."""
+        """Images in chunks whose largest activation stays within 2^30 elements (the kernels' per-operand 32-bit
+        element offsets).  Up block j of the decoder ends in an upsampler whose output keeps its rev[j] channels at
+        4^(j+1) times the latent pixels (rev = block_out_channels reversed); the largest of those, and of the mid
+        block's [h, w, rev[0]], bounds every activation of an image: SDXL [n, 8h, 8w, 256] -> 4 images per chunk at
+        1024^2."""
         B, h, w, _ = zp.shape
-        per = max(1, (1 << 30) // (64 * h * w * max(self.cfg.block_out_channels)))
+        rev = list(reversed(self.cfg.block_out_channels))
+        per_img = max([h * w * rev[0]] + [4 ** (j + 1) * h * w * rev[j] for j in range(len(rev) - 1)])
+        per = max(1, (1 << 30) // per_img)
         if B <= per:
             return self._decode_chunk(zp)
         out = torch.empty((B, 8 * h, 8 * w, self.cfg.out_channels), device=zp.device, dtype=BF16)

@@ -57,9 +57,10 @@ def test_gloo_world2_grad_sync_and_timing():
         assert t == 1.5
 
 
-def _bucket_worker(rank, world, port, q):
+def _bucket_worker(rank, world, port, q, wire=None):
     """GradBuckets on a fake 5-unit backward: buckets fire as their last unit completes, in completion order, and
-    the bucketed sum equals the flat all-reduce."""
+    the bucketed sum equals the flat all-reduce (bf16 wire: within the bf16 rounding of the two summands and the
+    sum, and every element is the bf16 sum cast back)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -74,7 +75,7 @@ def _bucket_worker(rank, world, port, q):
         flat = torch.randn(1024)
         expect = flat.clone()
         dist.all_reduce(expect)
-        gb = GradBuckets(FakeUNet(), flat, bucket_mb=400 * 4 / 1e6)   # 400-element buckets
+        gb = GradBuckets(FakeUNet(), flat, bucket_mb=400 * 4 / 1e6, wire_dtype=wire)   # 400-element buckets
         spans = [(o, n) for o, n, _ in gb.buckets]
         rt = type("RT", (), {})()
         done = gb.hook(rt)
@@ -83,18 +84,26 @@ def _bucket_worker(rank, world, port, q):
             done(u)
             issued.append(sum(w is not None for w in gb.works))
         scale = gb.finish()
-        q.put((rank, spans, issued, torch.equal(flat, expect), scale))
+        if wire is None:
+            ok = torch.equal(flat, expect)
+        else:
+            # bf16 rounding of the summands and of the sum (per element relative to the summands, so cancelling sums
+            # can be far off relatively): rel-L2 over the vector
+            ok = ((flat - expect).norm() / expect.norm()).item() < 1e-2 and torch.equal(flat, flat.to(wire).float())
+            assert gb.bytes_on_wire() == 1024 * 2
+        q.put((rank, spans, issued, ok, scale))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_gloo_world2_bucketed_overlap_sync():
+@pytest.mark.parametrize("wire", [None, torch.bfloat16])
+def test_gloo_world2_bucketed_overlap_sync(wire):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in range(world)]
@@ -136,3 +145,36 @@ def test_single_process_sync_is_identity():
     from pairwise_sample_optimization_amd.trainer import allreduce_grads
     g = torch.ones(3)
     assert allreduce_grads(g) == 1.0 and torch.equal(g, torch.ones(3))
+
+
+def _flat_bf16_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pairwise_sample_optimization_amd.trainer import allreduce_grads
+        torch.manual_seed(rank)
+        g = torch.randn(777)
+        expect = g.clone()
+        dist.all_reduce(expect)
+        scale = allreduce_grads(g, wire_dtype=torch.bfloat16)
+        q.put((scale, ((g - expect).norm() / expect.norm()).item() < 1e-2, g.dtype == torch.float32))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_flat_allreduce_bf16_wire():
+    """The un-bucketed sync (hipGraph epochs) with a bf16 wire: fp32 gradient in, fp32 sum out, bf16-close."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_flat_bf16_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    for scale, close, f32 in res:
+        assert scale == 0.5 and close and f32

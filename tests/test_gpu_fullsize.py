@@ -104,6 +104,8 @@ def _oracle_window(unet_sd, mb, tr, cfg, lora_leaf=None, param_leaf=None, ref_sd
                             for s in range(count)])
     (losses16.sum() / tr.gas_total).backward()
     loss16 = losses16.mean().item()
+    lps = SimpleNamespace(lpp=lpp.detach(), lpr=lpr.detach(), lpp16=l16.detach(), lpr16=r16.detach(), ep16=ep16,
+                          er16=er16, pref=pref)
     if grads16 is not None:  # the bf16 run's parameter gradients, image by image
         # fp32 leaves holding the bf16 values: autocast casts them for every conv / linear exactly as it does the
         # bf16 module weights, and the norms run in fp32 either way, so the activations match the bf16-weight run
@@ -123,7 +125,7 @@ def _oracle_window(unet_sd, mb, tr, cfg, lora_leaf=None, param_leaf=None, ref_sd
         (out * g_eps[i:i + 1]).sum().backward()
         del out
         print(f"  oracle backward image {i + 1}/{n}", flush=True)  # progress (the fp32 oracle takes minutes)
-    return ep, er, losses.mean().item(), loss16
+    return ep, er, losses.mean().item(), loss16, lps
 
 
 def _window(tr, buf, g):
@@ -133,16 +135,23 @@ def _window(tr, buf, g):
 
 
 def test_c2_turbo_lora_window_at_1024(cuda):
+    """The C2 window at 1024^2 with a LoRA large enough that the window loss leaves log 2 by far more than the bf16
+    noise, and the LoRA EFFECT itself asserted: delta = eps_pol - eps_ref of every image and the per-image log-ratio
+    Delta = lp_theta - lp_ref (the quantity beta = 50 amplifies, T:844-850) against the fp32 oracle's, each relative to
+    its own magnitude, next to the torch-bf16 run's distance.  Every bar is then checked to REJECT the LoRA-off path
+    (adapters disabled: delta = 0, Delta = 0, loss = log 2 exactly), which is also run."""
     from oracle import sdxl_ref
     from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
     from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    from pairwise_sample_optimization_amd import kernels as K
     h, P, gas, N, r = 128, 2, 2, 2, 32
     cfg = UNetConfig.sdxl(h)
     with torch.device(cuda):
         unet = UNet2DConditionModel(cfg)
     unet.init_weights(0)
     unet.add_adapter(SimpleNamespace(r=r, lora_alpha=r))
-    unet.lora.init_gaussian(seed=0, b_std=2e-3)  # LoRA effect a few % of eps: the loss is not log 2
+    # B std 6e-3: delta ~ 10 % of eps, |Delta| ~ 1e-2 (inside the clip range log(1 +- 0.1)), beta*Delta ~ 0.5
+    unet.lora.init_gaussian(seed=0, b_std=6e-3)
     unet.prepare()
     tr = PSOTrainer(unet, mode="turbo", num_steps=N, gradient_accumulation_steps=gas, train_batch_size=P)
     tr.auto_step = False
@@ -158,8 +167,16 @@ def test_c2_turbo_lora_window_at_1024(cuda):
     assert n == 8  # the bench's window: 4 pairs -> 8 policy + 8 reference images in ONE paired pass
     with torch.no_grad():
         eps_both, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False, paired_ref=True)
-    from pairwise_sample_optimization_amd import kernels as K
+        unet.disable_adapters()  # the LoRA-off path: what a build whose LoRA tail is lost would compute
+        eps_off, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
+        unet.enable_adapters()
     e_pol, e_ref = K.nhwc_to_nchw(eps_both[:n]), K.nhwc_to_nchw(eps_both[n:])
+    pref_k = K.preference(mb.rewards, 0)
+    ws = K.pair_loss_ws(n // 2, mb.x[0].numel(), cuda)
+    _, lp_mine = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[:n].contiguous(), eps_both[n:].contiguous(),
+                                 mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
+    loss_off, lp_off = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_off, eps_off, mb.coef, pref_k, tr.beta,
+                                       tr.clip_eps, ws)
     st = unet.lora
     st.grad.zero_()
     mine_loss = tr.micro_step(mb).item()
@@ -167,26 +184,52 @@ def test_c2_turbo_lora_window_at_1024(cuda):
     sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
     leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
     g16 = {}
-    ep, er, ref_loss, loss16 = _oracle_window(sd, mb, tr, cfg, lora_leaf=leaf, grads16=g16)
+    ep, er, ref_loss, loss16, lps = _oracle_window(sd, mb, tr, cfg, lora_leaf=leaf, grads16=g16)
     rp, rr = _rel(e_pol, ep), _rel(e_ref, er)
+    # the LoRA effect: delta = eps_pol - eps_ref per image (bf16-rounded eps, as the step functions see them)
+    d32 = ep.bfloat16().float() - er.bfloat16().float()
+    d16 = lps.ep16.bfloat16().float() - lps.er16.bfloat16().float()
+    rd, rd16 = _rel(e_pol - e_ref, d32), _rel(d16, d32)
+    eff = (d32.norm() / ep.norm()).item()
+    # per-image log-ratio Delta_i = lp_theta - lp_ref (row 2p + k of the window), mine vs fp32 vs torch-bf16
+    D32 = (lps.lpp - lps.lpr).reshape(-1)
+    D16 = (lps.lpp16 - lps.lpr16).reshape(-1)
+    Dm = (lp_mine[:, 0] - lp_mine[:, 1]).reshape(-1)
+    rD, rD16 = _rel(Dm, D32), _rel(D16, D32)
     rel = abs(mine_loss - ref_loss) / abs(ref_loss)
     rel16 = abs(loss16 - ref_loss) / abs(ref_loss)
     den = sum((v.grad ** 2).sum().item() for v in leaf.values())
     grel = (sum(((mine[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
     grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
-    print(f"C2 @1024: eps rel pol {rp:.2e} ref {rr:.2e}; loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} "
-          f"torch-bf16 {loss16:.6f} rel(mine) {rel:.2e} rel(torch-bf16) {rel16:.2e}; LoRA grad rel mine {grel:.3e} "
+    print(f"C2 @1024: eps rel pol {rp:.2e} ref {rr:.2e}; LoRA effect |delta|/|eps| {eff:.3e}, delta rel mine "
+          f"{rd:.3e} torch-bf16 {rd16:.3e}; Delta fp32 {D32.tolist()} mine {Dm.tolist()} rel mine {rD:.3e} torch-bf16 "
+          f"{rD16:.3e}; loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} torch-bf16 {loss16:.6f} LoRA-off "
+          f"{loss_off.item():.6f} rel(mine) {rel:.2e} rel(torch-bf16) {rel16:.2e}; LoRA grad rel mine {grel:.3e} "
           f"torch-bf16 {grel16:.3e} over {len(leaf)} tensors")
     assert rp < 3e-2 and rr < 3e-2
-    assert rel <= 1.5 * rel16 + 2e-3
+    bar_d = 1.5 * rd16 + 2e-2
+    bar_D = 1.5 * rD16 + 2e-2
+    bar_l = 1.5 * rel16 + 2e-3
+    assert rd <= bar_d and rd < 0.3
+    assert rD <= bar_D and rD < 0.3
+    assert rel <= bar_l
     assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
+    # the bars discriminate: the LoRA-off path (run above) fails every one of them
+    assert torch.equal(lp_off[:, 0], lp_off[:, 1])                  # Delta = 0 exactly
+    assert abs(loss_off.item() - math.log(2)) < 1e-6                  # loss = log 2 exactly
+    assert abs(loss_off.item() - ref_loss) / abs(ref_loss) > 3 * bar_l, (loss_off.item(), ref_loss, bar_l)
+    assert 1.0 > 3 * bar_d and 1.0 > 3 * bar_D                        # delta = 0 / Delta = 0 are rel 1.0 away
+    assert (D32.abs() < math.log(1.1)).all()                          # inside the clip: the gradient flows
 
 
-def test_c3_dmd_full_unet_window_at_1024(cuda):
+@pytest.mark.parametrize("P", [1, 2])
+def test_c3_dmd_full_unet_window_at_1024(cuda, P):
+    """C3 (P = 1, one GPU) and C4's per-rank workload (P = 2 pairs per GPU of the 8-GPU global 16, D:777-864): the
+    DMD2 full-UNet window (T = 3 micro-steps, 6P images in one pass) vs the fp32 oracle."""
     from oracle import sdxl_ref
     from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
     from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
-    h, P, gas, N = 128, 1, 1, 4
+    h, gas, N = 128, 1, 4
     cfg = UNetConfig.sdxl(h)
 
     def make():
@@ -216,14 +259,14 @@ def test_c3_dmd_full_unet_window_at_1024(cuda):
     buf = tr.sample_pairs(enc, pooled, tid, h, generator=g,
                           reward_fn=lambda img: torch.rand(img.shape[0], device=cuda, generator=g))
     mb = _window(tr, buf, g)
-    assert mb.unet_in.shape[0] == 6  # T = 3 micro-steps x 1 pair x 2 members
+    assert mb.unet_in.shape[0] == 6 * P  # T = 3 micro-steps x P pairs x 2 members
     fg.grad.zero_()
     mine_loss = tr.micro_step(mb).item()
     mine = {unet._unmap_key(nm): fg.g(p) for nm, p in unet.named_parameters()}
     sd_ref = sdxl_ref.sd_to(ref_unet.state_dict(), cuda)
     leaf = {k: v.clone().requires_grad_(True) for k, v in sdxl_ref.sd_to(unet.state_dict(), cuda).items()}
     g16 = {}
-    _, _, ref_loss, loss16 = _oracle_window(None, mb, tr, cfg, param_leaf=leaf, ref_sd=sd_ref, grads16=g16)
+    _, _, ref_loss, loss16, _ = _oracle_window(None, mb, tr, cfg, param_leaf=leaf, ref_sd=sd_ref, grads16=g16)
     rel = abs(mine_loss - ref_loss) / abs(ref_loss)
     rel16 = abs(loss16 - ref_loss) / abs(ref_loss)
     num = den = 0.0
@@ -238,7 +281,7 @@ def test_c3_dmd_full_unet_window_at_1024(cuda):
     grel = (num / den) ** 0.5
     grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
     worst.sort(reverse=True)
-    print(f"C3 @1024: loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} torch-bf16 {loss16:.6f} rel(mine) {rel:.2e} "
+    print(f"C3 @1024 P={P}: loss mine {mine_loss:.6f} fp32 {ref_loss:.6f} torch-bf16 {loss16:.6f} rel(mine) {rel:.2e} "
           f"rel(torch-bf16) {rel16:.2e}; full grad rel mine {grel:.3e} torch-bf16 {grel16:.3e} over {len(leaf)} "
           f"tensors; worst {worst[:3]}")
     assert len(leaf) == len(mine) == 1680

@@ -59,3 +59,29 @@ def test_lora_safetensors_format(tmp_path):
     got, alphas = lora_io.lora_state_dict(str(tmp_path))
     assert alphas is None
     assert torch.equal(lora_io.diffusers_to_peft(got)["a.attn1.to_q.lora_B.weight"], sd["a.attn1.to_q.lora_B.weight"])
+
+
+def test_trainer_from_config_latent_dtype_follows_mixed_precision():
+    """DMD2 from the reference config: latents (and so the step / log-prob arithmetic) in weight_dtype, as D:329-333
+    and DP/sdxl_dmd_with_logprob.py:91-101 make them; turbo always fp32 (DP/turbo_inference_with_logprob.py:69)."""
+    import warnings
+    from pairwise_sample_optimization_amd.config import config_sdxl_dmd_dpo
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer
+    seen = {}
+
+    class Probe(PSOTrainer):
+        def __init__(self, unet, **kw):  # capture what from_config resolves, build nothing
+            seen.update(kw)
+
+    c = config_sdxl_dmd_dpo.get_config()
+    for mp, want in (("fp16", torch.float16), ("bf16", torch.bfloat16), ("no", torch.float32)):
+        c.mixed_precision = mp
+        Probe.from_config(None, c, mode="dmd")
+        assert seen["latent_dtype"] == want, (mp, seen["latent_dtype"])
+        Probe.from_config(None, c, mode="turbo")
+        assert seen["latent_dtype"] == torch.float32
+    c.mixed_precision = "fp16"
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        Probe.from_config(None, c, mode="dmd", latent_dtype=torch.float32)
+    assert seen["latent_dtype"] == torch.float32 and any("mixed_precision" in str(x.message) for x in w)
