@@ -157,6 +157,21 @@ int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, lon
  * restricted to j in that group's r columns (out is [I][r]).  group = 0: plain pso_gemm_tn. */
 int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                         long ldo, int group, void* stream);
+/* Batched rank-r TN products (the LoRA weight gradients of one gradient unit, deferred to the unit's end and issued
+ * as ONE launch per rank / orientation instead of one launch each; same arithmetic as pso_gemm_tn).  Problem i:
+ *   out_jc = 0 (dB = s dY^T u):  out[c][j]  += alpha * sum_m x[m][c] * u[m][(c / group_c) * R + j]   (out [C][R])
+ *   out_jc = 1 (dA = v^T x):     out[j][c]  += alpha * sum_m x[m][c] * u[m][j]                       (out [R][C])
+ * with x [M][C] (C % 128 == 0) the activation / output-gradient stream and u [M][*] the rank-R projection
+ * (R = 32, 64 or 96), group_c = 0 or a multiple of 128 dividing C (the fused q/k/v adapters).  f32 atomics into
+ * out; probs is HOST memory, copied into the launch arguments (capturable in a hipGraph). */
+typedef struct {
+  const void* x; long ldx;
+  const void* u; long ldu;
+  float* out; long ldo;
+  int M, C, group_c;
+  float alpha;
+} PsoTnRankProblem;
+int pso_gemm_tn_rank_batch(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* stream);
 /* Grouped (block-diagonal) skinny product for the fused q/k/v LoRA adapters of the backward (v = dy sB per adapter):
  * out[m][g*N + n] = alpha * sum_k A[m][g*K + k] * W[n][g*K + k] for g < groups (bf16 out, N <= 128, N % 4 == 0). */
 int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,

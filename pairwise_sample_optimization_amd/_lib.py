@@ -22,6 +22,13 @@ COEF_STRIDE = 8
 
 _lib = None
 
+
+class PsoTnRankProblem(ctypes.Structure):
+    """include/pso_amd.h PsoTnRankProblem (one product of pso_gemm_tn_rank_batch)."""
+    _fields_ = [("x", ctypes.c_void_p), ("ldx", ctypes.c_long), ("u", ctypes.c_void_p), ("ldu", ctypes.c_long),
+                ("out", ctypes.c_void_p), ("ldo", ctypes.c_long), ("M", ctypes.c_int), ("C", ctypes.c_int),
+                ("group_c", ctypes.c_int), ("alpha", ctypes.c_float)]
+
 vp = ctypes.c_void_p
 ci = ctypes.c_int
 cf = ctypes.c_float
@@ -61,6 +68,7 @@ SIGNATURES = {
     "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_gemm_tn_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
+    "pso_gemm_tn_rank_batch": (ci, [ci, ci, ci, vp, vp]),
     "pso_gemm_skinny_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
     "pso_gemm_geglu": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, vp, cl, vp, cl, ci, vp]),
     "pso_gemm_geglu_bwd": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp]),

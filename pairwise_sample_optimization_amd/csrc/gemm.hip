@@ -771,6 +771,9 @@ int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const 
 int pso_gemm8p160_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
                       int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
                       const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st);
+int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
+                      int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
+                      const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 static int g_gemm_variant = 0;
@@ -785,7 +788,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
-  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38) ? 0 : gv_raw;
+  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39) ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
@@ -849,6 +852,13 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (ok160 && gv_raw != 37 && (gv_raw == 38 || (gv == 0 && t160 >= 256 && Ktot >= 2560)))
     return pso_gemm8p160_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
+  // 8-phase 256 x 320 (gemm8p.hip): every SDXL width is a multiple of 320, and at the UNet's M (256 * 2^k rows) the
+  // tile count is a whole number of 256-CU rounds (N = 1280 at M = 16384: 256 tiles; N = 640 at M = 65536: 512).
+  // Variant 39 forces it where it applies (A/B knob).
+  const bool ok320 = base8 && (g.N % 320) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
+  if (ok320 && gv_raw == 39) return pso_gemm8p320_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2,
+                                                      g.b2, g.ldb2, g.tail_m, g.tail_group_n, g.alpha, g.bias, g.resid,
+                                                      g.ldr, g.out, g.ldo, g.group_m, st);
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);

@@ -95,15 +95,18 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 // row pitch.  Plain epilogue only, bf16 only.
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
-  static_assert(BN == 256 || (BN == 160 && EPI == EPI8_NONE && !FP8), "256 x 160 tiles: plain bf16 epilogue only");
+  static_assert(BN == 256 || ((BN == 160 || BN == 320) && EPI == EPI8_NONE && !FP8),
+                "256 x 160 / 256 x 320 tiles: plain bf16 epilogue only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
-  constexpr int BH0 = BN == 256 ? 128 : 96, BH1 = BN - BH0;  // rows of the two B images
+  constexpr int BH0 = BN == 256 ? 128 : (BN == 320 ? 160 : 96), BH1 = BN - BH0;  // rows of the two B images
   constexpr int MI = 2;                                       // row subtiles per wave (32 rows of a 128-row half)
   constexpr int CW0 = BH0 / 2, CW1 = BH1 / 2;                 // columns per wave in the B0 / B1 quadrants
   constexpr int NJ0 = CW0 / 16, NJ1 = CW1 / 16, NJ = NJ0;     // column subtiles per wave
   constexpr int BUFE = 2 * HT + BN * 64;                      // elements of one K-tile buffer [A0 A1 B0 B1]
-  constexpr int BW0 = BH0 / 16, BW1 = BH1 / 16;               // waves staging B0 / B1 (2 pieces each)
+  constexpr int BW0 = BH0 / 16, BW1 = BH1 / 16;               // waves staging B0 / B1 (2 pieces each; 320: XP)
+  // 256 x 320: a 160-row B image is 20 pieces -- pieces 2w, 2w+1 for every wave plus piece 16 + w for waves 0-3
+  constexpr bool XP = BN == 320;
   extern __shared__ __attribute__((aligned(16))) bf16_t l8[];  // [2 bufs][A0 A1 B0 B1]
   const int tid = threadIdx.x, lane = tid & 63;
   // wave index in an SGPR: the LDS-DMA destinations (M0) are then scalar arithmetic, not 8 spilled VGPR addresses
@@ -149,17 +152,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // offset (64-bit per-lane pointers for the 8 source rows spill at this register budget, and a spill reload's
   // vmcnt(0) would drain the whole ring).
   const int prow = lane >> 3, pch = lane & 7;
-  unsigned aoff[2][2], woff[2][2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int R = (wave * 2 + i) * 8 + prow;
-      const int lc = pch ^ (R & 7);
-      aoff[h][i] = (unsigned)(min(m0 + h * 128 + R, g.M - 1) * (int)g.lda * ES + lc * 16);
-      woff[h][i] = (unsigned)((n0 + h * BH0 + min(R, (h ? BH1 : BH0) - 1)) * (int)g.ldw * ES + lc * 16);
-    }
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
+  // Every piece is 8 rows x 128 B, so a lane's row inside its piece is prow and its swizzled source chunk pch ^ prow
+  // for every piece: the per-lane part of a staging offset is ONE register per operand (vA / vW); the piece's row
+  // base, the half and the K-tile advance are wave-uniform and go in the scalar soffset.  Rows past M read as zeros
+  // through rA's range (they are never stored), so no per-lane clamp is needed.
+  const unsigned vA = (unsigned)(prow * (int)g.lda * ES + (pch ^ prow) * 16);
+  const unsigned vW = (unsigned)(prow * (int)g.ldw * ES + (pch ^ prow) * 16);
+  // row (inside its image) of this lane in B piece i of this wave (LoRA tail path)
+  auto bpiece_row = [&](int i) { return (i < 2 ? wave * 2 + i : 16 + wave) * 8 + prow; };
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)((long)g.M * g.lda * ES), 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rA2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.a2 ? g.a2 : g.a), (short)0, 0x7fffffff, 0x00020000);
@@ -172,31 +174,44 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   auto stage = [&](int kt, int img) {
     const int half = img & 3;
     bf16_t* dst = l8 + img_off(img) + wave * 2 * 8 * 64;
-    if (BN != 256 && half >= 2 && wave >= (half == 2 ? BW0 : BW1)) return;  // 96 / 64-row B images: waves 0-5 / 0-3
+    if (BN == 160 && half >= 2 && wave >= (half == 2 ? BW0 : BW1)) return;  // 96 / 64-row B images: waves 0-5 / 0-3
+    // the extra (third) B piece of waves 0-3 in the 256 x 320 form: piece 16 + w of the image
+    bf16_t* dst_x = l8 + img_off(img) + (16 + wave) * 8 * 64;
+    const bool xp = XP && half >= 2 && wave < 4;
     if (kt < nt1) {
-      const unsigned k0 = (unsigned)kt * 128u;  // bytes
+      const int k0 = kt * 128;  // bytes
       if (half < 2) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, aoff[half][0] + k0, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, aoff[half][1] + k0, 0, 0, 0);
+        const int sa = (m0 + (half & 1) * 128 + wave * 16) * (int)g.lda * ES + k0;  // piece 2w, row 0
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, vA, sa, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, vA, sa + 8 * (int)g.lda * ES, 0, 0);
       } else {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, woff[half - 2][0] + k0, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, woff[half - 2][1] + k0, 0, 0,
+        const int sw = (n0 + (half & 1) * BH0 + wave * 16) * (int)g.ldw * ES + k0;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, vW, sw, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, vW, sw + 8 * (int)g.ldw * ES, 0,
                                                  0);
+        if constexpr (XP)
+          if (xp)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rW, (lds8_void*)dst_x, 16, vW, (n0 + (half & 1) * BH0 + (16 + wave) * 8) * (int)g.ldw * ES + k0, 0, 0);
       }
     } else {  // LoRA K-tail (one or two K-tiles per output tile) or the zero pad tile
       const int kc = (kt - nt1) * KT + (pch ^ prow) * (16 / ES);  // this lane's 16-B chunk of the tail
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int R = (half & 1) * (half < 2 ? 128 : BH0) + (wave * 2 + i) * 8 + prow;
+      for (int i = 0; i < (XP ? 3 : 2); ++i) {
+        if (i == 2 && !xp) break;
         unsigned off;
         if (half < 2) {
+          if (i == 2) break;
+          const int R = (half & 1) * 128 + (wave * 2 + i) * 8 + prow;
           const int m = m0 + R;
           off = (kin && m < g.tail_m) ? (unsigned)(((long)m * g.lda2 + a2_col + kc) * ES) : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rA2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
         } else {
+          const int R = (half & 1) * BH0 + bpiece_row(i);
           off = kin ? (unsigned)(((long)(n0 + R) * g.ldw2 + kc) * ES) : OOB;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW2, (lds8_void*)(dst + i * 8 * 64), 16, off, 0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW2, (lds8_void*)(i == 2 ? dst_x : dst + i * 8 * 64), 16, off, 0,
+                                                   0, 0);
         }
       }
     }
@@ -221,21 +236,20 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   typedef __attribute__((ext_vector_type(4))) int i32x4_t;
   typedef __attribute__((address_space(3))) const i32x4_t lds_frag4;
   const unsigned l8base = (unsigned)(uintptr_t)(lds8_void*)l8;
-  unsigned la[2], lb[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    // bf16: 8-element chunk kk*4 + fk (k = 32 kk + 8 fk ..); fp8: the lane's 32 consecutive k are chunks 2 fk, 2 fk + 1
-    const int ch = FP8 ? 2 * fk + kk : kk * 4 + fk;
-    la[kk] = (unsigned)swz8(wr * 32 + fr, ch) * 2u;
-    lb[kk] = (unsigned)swz8(fr, ch) * 2u;  // + the wave's column offset wc * CW rows (a multiple of 8: same swizzle)
-  }
+  // ONE lane register serves every fragment read: bf16 chunk kk*4 + fk (k = 32 kk + 8 fk ..), fp8 chunks 2 fk + kk
+  // (the lane's 32 consecutive k), so kk = 1 is the kk = 0 offset with byte bit 6 (bf16) / bit 4 (fp8) flipped; the
+  // A images' row offset wr * 32 keeps the swizzle (a multiple of 8 rows) and is wave-uniform, like the B images'
+  // column offset wc * CW rows
+  const unsigned lb0 = (unsigned)swz8(fr, FP8 ? 2 * fk : fk) * 2u;
+  constexpr unsigned KKX = FP8 ? 16u : 64u;
   i32x4_t ta[2], tb[4];
   auto read_a = [&](int img) {
-    const unsigned ib = l8base + (unsigned)(img_off(img) * 2);
+    const unsigned ib = l8base + (unsigned)(img_off(img) * 2) + (unsigned)(wr * 32 * 128);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned ad;
-      asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(la[kk]));
+      if (kk == 0) asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb0));
+      else asm volatile("v_xor_b32 %0, %1, %2\n\tv_add_u32 %0, %3, %0" : "=&v"(ad) : "v"(lb0), "n"(KKX), "s"(ib));
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if constexpr (FP8) {
@@ -253,7 +267,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned ad;
-      asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb[kk]));
+      if (kk == 0) asm volatile("v_add_u32 %0, %1, %2" : "=v"(ad) : "s"(ib), "v"(lb0));
+      else asm volatile("v_xor_b32 %0, %1, %2\n\tv_add_u32 %0, %3, %0" : "=&v"(ad) : "v"(lb0), "n"(KKX), "s"(ib));
 #pragma unroll
       for (int j = 0; j < (hb ? NJ1 : NJ0); ++j) {
         if constexpr (FP8) {
@@ -320,18 +335,34 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < (hb ? NJ1 : NJ0); ++j)
-            acc[ha][hb][i][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
+          for (int j = 0; j < (hb ? NJ1 : NJ0); ++j) {
+            if constexpr (BN == 320)  // accumulator tied in place (the builtin form double-buffers and spills here)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[ha][hb][i][j]) : "v"(bfr[j][kk]),
+                           "v"(af[i][kk]));
+            else
+              acc[ha][hb][i][j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[ha][hb][i][j], 0, 0, 0);
+          }
+      if constexpr (BN == 320)  // the asm MFMAs are invisible to the hazard recognizer: see the FP8 form's note
+        asm volatile("s_nop 7"
+                     : "+v"(acc[ha][hb][0][0]), "+v"(acc[ha][hb][0][1]), "+v"(acc[ha][hb][0][2]),
+                       "+v"(acc[ha][hb][0][3]), "+v"(acc[ha][hb][0][4]), "+v"(acc[ha][hb][1][0]),
+                       "+v"(acc[ha][hb][1][1]), "+v"(acc[ha][hb][1][2]), "+v"(acc[ha][hb][1][3]),
+                       "+v"(acc[ha][hb][1][4]));
     }
     if (!SPRIO) __builtin_amdgcn_s_setprio(0);
   };
   // the counted wait that retires all but the last three stagings (B0, A1, B1): 6 loads per wave, fewer for the waves
   // that stage no B1 (4) or no B pieces at all (2) in the 256 x 160 form
   auto vm_wait6 = [&]() {
-    if (BN == 256 || wave < BW1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (wave < BW0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if constexpr (BN == 320) {  // waves 0-3 stage 3 pieces per B image: 3 + 2 + 3 in flight, the others 2 + 2 + 2
+      if (wave < 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      if (BN == 256 || wave < BW1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (wave < BW0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
   };
   // one phase: reads (RA / RB: which operand image to (re)load), the stage (if its K-tile exists), the optional
   // counted wait (VM: -1 none, else vmcnt(VM)), barrier, MFMAs of quadrant (HA, HB), barrier.
@@ -376,7 +407,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   }
 #undef PHASE
   // FP8: the inline-asm MFMAs are invisible to the hazard recognizer -- pad before any VALU reads an accumulator
-  if constexpr (FP8) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  if constexpr (FP8 || BN == 320) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   if (STAG && wave < 4) __builtin_amdgcn_s_barrier();
   if (SPRIO) __builtin_amdgcn_s_setprio(0);
 
@@ -392,7 +423,77 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
           for (int j = 0; j < (b ? NJ1 : NJ0); ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
     goto tile_end;
   }
-  if constexpr (BN == 160) {
+  if constexpr (BN == 320) {
+    // 256 x 320 tile through LDS in two 128-row halves (the whole tile would need 160 KB): rows at a 328-element
+    // (656-B = 164-dword) pitch -- the ds_write_b64 of a 16-row fragment column hits 16 distinct bank pairs -- read
+    // back as 40 16-B chunks per row and stored whole (640 B).  Register budget: the 160 accumulator registers are
+    // live until a half is staged, so the bias is loaded per column half (20 registers) and the residual chunks only
+    // once the half's accumulators are in LDS.
+    __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
+    constexpr int TP = 328;
+    bf16_t* tl = l8;
+    const bool has_r = g.resid != nullptr;
+    auto stage_half = [&](auto HA_) {
+      constexpr int ha = decltype(HA_)::value;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        float bv[NJ][4];
+#pragma unroll
+        for (int jt = 0; jt < NJ; ++jt) {
+          const int n = n0 + hb * BH0 + wc * CW0 + jt * 16 + fk * 4;
+          const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
+          bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
+          bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int R = wr * 32 + i * 16 + fr;
+#pragma unroll
+          for (int jt = 0; jt < NJ; ++jt) {
+            const int col = hb * BH0 + wc * CW0 + jt * 16 + fk * 4;
+            const f32x4 a = acc[ha][hb][i][jt];
+            const float al = g.alpha;
+            *reinterpret_cast<uint2*>(tl + R * TP + col) =
+                make_uint2(pack2bf(a[0] * al + bv[jt][0], a[1] * al + bv[jt][1]),
+                           pack2bf(a[2] * al + bv[jt][2], a[3] * al + bv[jt][3]));
+          }
+        }
+      }
+    };
+    auto store_half = [&](int ha) {
+      uint4 rvp[10];
+#pragma unroll
+      for (int p = 0; p < 10; ++p) {
+        const int idx = p * 512 + tid;
+        const int R = idx / 40, c = idx - R * 40, m = min(m0 + ha * 128 + R, g.M - 1);
+        rvp[p] = has_r ? *reinterpret_cast<const uint4*>(g.resid + (long)m * g.ldr + n0 + c * 8) : make_uint4(0, 0, 0, 0);
+      }
+      // LDS-only barrier: the residual loads stay in flight across it
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < 10; ++p) {  // 128 rows x 40 chunks = 10 passes of 512
+        const int idx = p * 512 + tid;
+        const int R = idx / 40, c = idx - R * 40, m = m0 + ha * 128 + R;
+        if (m >= g.M) continue;
+        uint4 y = *reinterpret_cast<const uint4*>(tl + R * TP + c * 8);
+        if (has_r) {  // residual added to the bf16-rounded projection (the unfused Linear + add)
+          const uint4 rv = rvp[p];
+          const uint32_t yw[4] = {y.x, y.y, y.z, y.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = pack2bf(bf2f(yw[e] & 0xffff) + bf2f(rw[e] & 0xffff), bf2f(yw[e] >> 16) + bf2f(rw[e] >> 16));
+          y = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 + c * 8) = y;
+      }
+    };
+    stage_half(ic8<0>{});
+    store_half(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the first half's LDS reads retired
+    stage_half(ic8<1>{});
+    store_half(1);
+  } else if constexpr (BN == 160) {
     // 256 x 160 tile through LDS at a 168-element (336-B) row pitch: the ds_write_b64 of a 16-row fragment column hits
     // 16 distinct bank pairs (84 dwords per row), rows are read back as 20 16-B chunks and stored whole (320 B)
     __builtin_amdgcn_s_waitcnt(0xC07F & ~0x3F00);  // lgkmcnt(0): this wave's LDS traffic retired
@@ -599,6 +700,7 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
   }
   if (FP8) pso_note_kernel("gemm8p_kernel<%d, true, false, true>", EPI);
   else if (BN == 160) pso_note_kernel("gemm8p_kernel<0, true, false, false, 160>");
+  else if (BN == 320) pso_note_kernel("gemm8p_kernel<0, true, false, false, 320>");
   else pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
   gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(g);
   return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
@@ -654,6 +756,20 @@ int pso_gemm8p160_run(int M, int N, int K, const void* a, long lda, const void* 
   g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
   return launch8<EPI8_NONE, true, false, false, 160>(g, st);
+}
+
+// 256 x 320 tiles (N % 320 == 0, K % 64 == 0, plain epilogue; preconditions checked in gemm.hip)
+int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
+                      int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
+                      const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st) {
+  Gemm8Args g{};
+  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
+  g.M = M; g.N = N; g.K = K;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0; g.w2 = (const bf16_t*)w2; g.ldw2 = ldw2;
+  g.tail_m = tail_m; g.tail_group_n = a2 ? tail_group_n : 0;
+  g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  return launch8<EPI8_NONE, true, false, false, 320>(g, st);
 }
 
 // FP8 form (pso_amd.h, pso_gemm_fp8): staggered wave groups, epilogue 0 (bias / alpha / residual) or 1 (GEGLU)

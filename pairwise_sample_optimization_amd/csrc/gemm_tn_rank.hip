@@ -44,11 +44,36 @@ __device__ __forceinline__ bf16x8 tnr_frag(const bf16_t* img, int m0, int col0, 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Batched form: one launch runs many independent products (the LoRA dA / dB of every adapter of a gradient unit,
+// deferred until the unit's backward is done).  The problem table travels in the kernel arguments; workgroup b runs
+// problem p with blk0[p] <= b < blk0[p + 1] (a scalar scan over <= TNR_MAXP entries read straight from the kernarg
+// segment), so a small product no longer pays a launch, a ramp and a tail of its own.
+constexpr int TNR_MAXP = 32;
+struct TnrProb {
+  const bf16_t* x; long ldx;
+  const bf16_t* u; long ldu;
+  float* out; long ldo;
+  int M, C, group_c, spb;
+  float alpha; int blk0;
+};
+struct TnrBatch {
+  int count, nblk;
+  TnrProb p[TNR_MAXP];
+};
+
 template <int NJT, bool OUT_JC>
-__global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int M, int C, const bf16_t* __restrict__ X, long ldx,
-                                                              const bf16_t* __restrict__ U, long ldu, int group_c,
-                                                              float alpha, float* __restrict__ out, long ldo,
-                                                              int steps_per_block) {
+__global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(TnrBatch bt) {
+  int pi = 0;
+  for (int q = 1; q < bt.count; ++q)
+    if ((int)blockIdx.x >= bt.p[q].blk0) pi = q;
+  const TnrProb& pr_ = bt.p[pi];
+  const int M = pr_.M, C = pr_.C, group_c = pr_.group_c, steps_per_block = pr_.spb;
+  const bf16_t* __restrict__ X = pr_.x;
+  const bf16_t* __restrict__ U = pr_.u;
+  float* __restrict__ out = pr_.out;
+  const long ldx = pr_.ldx, ldu = pr_.ldu, ldo = pr_.ldo;
+  const float alpha = pr_.alpha;
+  const int lblk = (int)blockIdx.x - pr_.blk0;
   constexpr int R = 16 * NJT;
   constexpr int UIMG = (R + 63) / 64;
   constexpr int STG = 3;
@@ -58,7 +83,7 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, cl = lane & 15;
   const int ncb = C / 128;
-  const int cb = blockIdx.x % ncb, mb = blockIdx.x / ncb;
+  const int cb = lblk % ncb, mb = lblk / ncb;
   const int c0 = cb * 128;
   const int u_off = group_c > 0 ? (c0 / group_c) * R : 0;
   const int nsteps_all = (M + 63) / 64;
@@ -178,24 +203,46 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(int
 }
 
 template <int NJT>
-int launch_tnr(int M, int C, const bf16_t* X, long ldx, const bf16_t* U, long ldu, int group_c, float alpha, float* out,
-               long ldo, bool out_jc, hipStream_t st) {
-  const int ncb = C / 128;
-  const int nsteps = (M + 63) / 64;
-  // ~2 workgroups per CU, at least 3 steps each (two in flight behind the one being multiplied)
-  int nmb = (512 + ncb - 1) / ncb;
-  int spb = (nsteps + nmb - 1) / nmb;
-  if (spb < 3) spb = 3;
-  nmb = (nsteps + spb - 1) / spb;
-  const dim3 grid(ncb * nmb);
+int launch_tnr_batch(TnrBatch& bt, bool out_jc, hipStream_t st) {
+  if (bt.count == 0) return PSO_OK;
   if (out_jc) {
     pso_note_kernel("gemm_tn_rank_kernel<%d, true>", NJT);
-    gemm_tn_rank_kernel<NJT, true><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
+    gemm_tn_rank_kernel<NJT, true><<<bt.nblk, 256, 0, st>>>(bt);
   } else {
     pso_note_kernel("gemm_tn_rank_kernel<%d, false>", NJT);
-    gemm_tn_rank_kernel<NJT, false><<<grid, 256, 0, st>>>(M, C, X, ldx, U, ldu, group_c, alpha, out, ldo, spb);
+    gemm_tn_rank_kernel<NJT, false><<<bt.nblk, 256, 0, st>>>(bt);
   }
   return pso_check_launch("pso_gemm_tn(rank)");
+}
+
+// Row-steps per workgroup.  Each workgroup adds its 128 x R partial into the f32 output with atomics
+// (128 * R * 4 bytes at the chip's ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics") after
+// streaming spb * 64 rows of X (spb * 16 KB at ~6 TB/s): spb >= R / 4 keeps the atomics near a tenth of the stream.
+// Alone (one product per launch) the split is finer -- ~2 workgroups per CU -- and at least 3 steps (two in flight
+// behind the one being multiplied).
+static int tnr_spb(int M, int C, int R, bool batched) {
+  const int ncb = C / 128, nsteps = (M + 63) / 64;
+  int spb;
+  if (batched) {
+    spb = R / 4;
+  } else {
+    const int nmb = (512 + ncb - 1) / ncb;
+    spb = (nsteps + nmb - 1) / nmb;
+  }
+  if (spb < 3) spb = 3;
+  if (spb > nsteps) spb = nsteps;
+  return spb < 1 ? 1 : spb;
+}
+
+template <int NJT>
+int launch_tnr(int M, int C, const bf16_t* X, long ldx, const bf16_t* U, long ldu, int group_c, float alpha, float* out,
+               long ldo, bool out_jc, hipStream_t st) {
+  TnrBatch bt{};
+  const int spb = tnr_spb(M, C, 16 * NJT, false);
+  bt.count = 1;
+  bt.p[0] = TnrProb{X, ldx, U, ldu, out, ldo, M, C, group_c, spb, alpha, 0};
+  bt.nblk = (C / 128) * ((((M + 63) / 64) + spb - 1) / spb);
+  return launch_tnr_batch<NJT>(bt, out_jc, st);
 }
 
 }  // namespace
@@ -212,4 +259,45 @@ int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long 
     case 96: return launch_tnr<6>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
     default: pso_set_error("pso_gemm_tn(rank): R must be 32, 64 or 96"); return PSO_ERR_ARG;
   }
+}
+
+// Batched entry (pso_amd.h pso_gemm_tn_rank_batch): count products of one rank R and one orientation, in chunks of
+// TNR_MAXP per launch.
+extern "C" int pso_gemm_tn_rank_batch(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* stream) {
+  PSO_ARG_CHECK(R == 32 || R == 64 || R == 96, "pso_gemm_tn_rank_batch: R must be 32, 64 or 96 (R=%d)", R);
+  PSO_ARG_CHECK(count >= 0 && (count == 0 || probs), "pso_gemm_tn_rank_batch: bad problem list");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  for (int i = 0; i < count; ++i) {
+    const PsoTnRankProblem& q = probs[i];
+    PSO_ARG_CHECK(q.x && q.u && q.out && q.M >= 0 && q.C > 0 && (q.C % 128) == 0,
+                  "pso_gemm_tn_rank_batch: problem %d: need C %% 128 == 0 and non-null operands", i);
+    PSO_ARG_CHECK(al16(q.x) && al16(q.u) && (q.ldx % 8) == 0 && (q.ldu % 8) == 0,
+                  "pso_gemm_tn_rank_batch: problem %d: X / U need 16-B aligned rows", i);
+    PSO_ARG_CHECK(q.group_c == 0 || ((q.group_c % 128) == 0 && (q.C % q.group_c) == 0),
+                  "pso_gemm_tn_rank_batch: problem %d: group_c must divide C in multiples of 128", i);
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  int i = 0;
+  while (i < count) {
+    TnrBatch bt{};
+    int nblk = 0;
+    for (; i < count && bt.count < TNR_MAXP; ++i) {
+      const PsoTnRankProblem& q = probs[i];
+      if (q.M == 0) continue;
+      const int spb = tnr_spb(q.M, q.C, R, true);
+      const int nb = (q.C / 128) * ((((q.M + 63) / 64) + spb - 1) / spb);
+      bt.p[bt.count++] = TnrProb{(const bf16_t*)q.x, q.ldx, (const bf16_t*)q.u, q.ldu, q.out, q.ldo, q.M, q.C,
+                                 q.group_c, spb, q.alpha, nblk};
+      nblk += nb;
+    }
+    bt.nblk = nblk;
+    int rc;
+    switch (R) {
+      case 32: rc = launch_tnr_batch<2>(bt, out_jc != 0, st); break;
+      case 64: rc = launch_tnr_batch<4>(bt, out_jc != 0, st); break;
+      default: rc = launch_tnr_batch<6>(bt, out_jc != 0, st); break;
+    }
+    if (rc != PSO_OK) return rc;
+  }
+  return PSO_OK;
 }

@@ -247,6 +247,44 @@ def gemm_tn(a, b, out, alpha=1.0, group=0):
     return out
 
 
+class TnRankQueue:
+    """Deferred LoRA weight-gradient products (gemm_tn calls whose one side is a rank-32/64/96 projection).  The
+    backward records them as it goes (add) and issues them per gradient unit (flush) as ONE pso_gemm_tn_rank_batch
+    launch per (rank, orientation): the ~700 rank-r products of a C2 step become a few dozen launches, each with
+    enough workgroups to fill the chip, and fewer f32 atomics per byte streamed.  The queue holds a reference to
+    every operand until its launch, so the caching allocator cannot recycle them early.  Products the rank kernel
+    does not take run at once through gemm_tn (same arithmetic either way)."""
+
+    def __init__(self):
+        self.pending = {}  # (R, out_jc) -> [(problem, operands, flop, bytes)]
+
+    def add(self, a, b, out, alpha=1.0, group=0):
+        M, I = a.shape
+        J = b.shape[1]
+        r = J * group // I if group else J
+        assert b.shape[0] == M and out.shape == (I, r) and out.dtype == torch.float32
+        rk = lambda x: x in TN_RANKS
+        if I % 128 == 0 and (rk(J) if group == 0 else (group % 128 == 0 and I % group == 0 and rk(r))):
+            key, x, u, R, gc = (r, 0), a, b, r, group
+        elif J % 128 == 0 and group == 0 and rk(I):
+            key, x, u, R, gc = (I, 1), b, a, I, 0
+        else:
+            return gemm_tn(a, b, out, alpha, group)
+        require_cuda(x, u, out)
+        prob = _lib.PsoTnRankProblem(ptr(x), _row_stride(x), ptr(u), _row_stride(u), ptr(out), _row_stride(out),
+                                     M, x.shape[1], gc, float(alpha))
+        self.pending.setdefault(key, []).append((prob, (x, u, out), 2.0 * M * I * r, 2.0 * M * (I + J) + 8.0 * I * r))
+        return out
+
+    def flush(self):
+        for (R, ojc), items in self.pending.items():
+            arr = (_lib.PsoTnRankProblem * len(items))(*[it[0] for it in items])
+            e0 = _prof_begin()
+            check(lib().pso_gemm_tn_rank_batch(R, ojc, len(items), arr, stream_ptr()), "pso_gemm_tn_rank_batch")
+            _prof_end(e0, sum(it[2] for it in items), sum(it[3] for it in items), ("gemm_tn_batch", R, ojc, len(items)))
+        self.pending = {}
+
+
 def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=None, bias=None, rowbias=None,
            resid=None, a2=None, w2=None, alpha=1.0, out=None, out_dtype=BF16, accumulate=False):
     """NHWC implicit-GEMM conv.  x [B,H,W,C1] (+ x2 [B,H,W,C2] concatenated on channels); weight [Cout,ks,ks,C1+C2].

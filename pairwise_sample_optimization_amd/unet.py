@@ -20,6 +20,7 @@ MI355X-first design:
     accumulate into directly (f32-accumulate epilogue) -- the all-reduce bucket and the optimizer operand.
 """
 import math
+import os
 from dataclasses import dataclass, field, replace
 from types import SimpleNamespace
 
@@ -29,6 +30,8 @@ import torch.nn as nn
 from . import kernels as K
 
 BF16 = torch.bfloat16
+# batched (per gradient unit) LoRA weight-gradient launches; PSO_TN_BATCH=0 issues every product at once (A/B knob)
+TN_BATCH = os.environ.get("PSO_TN_BATCH", "1") != "0"
 
 
 # ======================================================================================================================
@@ -532,7 +535,7 @@ class BasicTransformerBlock(nn.Module):
             v_o2 = K.gemm(dh2, L.sBt_o2)
             da2 = K.gemm(dh2, o2.wt, a2=v_o2, w2=L.At_o2)
             a2s, uo2 = sv["a2"], sv["u_o2"]
-            rt.side.launch(lambda: (K.gemm_tn(v_o2, a2s, g("attn2.A_o")), K.gemm_tn(dh2, uo2, g("attn2.B_o"), st.scale)),
+            rt.side.launch(lambda: (rt.dw(v_o2, a2s, g("attn2.A_o")), rt.dw(dh2, uo2, g("attn2.B_o"), st.scale)),
                            v_o2, a2s, dh2, uo2)
         else:
             da2 = K.gemm(dh2, o2.wt)
@@ -552,17 +555,17 @@ class BasicTransformerBlock(nn.Module):
             n2s, uq2, enc_, u_kv2 = sv["n2"], sv["u_q2"], rt.enc, sv["u_kv2"]
 
             def dw_attn2():
-                K.gemm_tn(v_q2, n2s, g("attn2.A_q"))
-                K.gemm_tn(dq2, uq2, g("attn2.B_q"), st.scale)
+                rt.dw(v_q2, n2s, g("attn2.A_q"))
+                rt.dw(dq2, uq2, g("attn2.B_q"), st.scale)
                 # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
                 v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
-                K.gemm_tn(v_kv, enc_, g("attn2.A_kv"))
+                rt.dw(v_kv, enc_, g("attn2.A_kv"))
                 gB = g("attn2.B_kv")
                 if r in K.TN_RANKS:
-                    K.gemm_tn(dkv2, u_kv2, gB, st.scale, group=C)
+                    rt.dw(dkv2, u_kv2, gB, st.scale, group=C)
                 else:
-                    K.gemm_tn(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
-                    K.gemm_tn(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
+                    rt.dw(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
+                    rt.dw(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
             rt.side.launch(dw_attn2, v_q2, n2s, dq2, uq2, dkv2, enc_, u_kv2)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
@@ -578,7 +581,7 @@ class BasicTransformerBlock(nn.Module):
             v_o1 = K.gemm(dh1, L.sBt_o1)
             da1 = K.gemm(dh1, o1.wt, a2=v_o1, w2=L.At_o1)
             a1s, uo1 = sv["a1"], sv["u_o1"]
-            rt.side.launch(lambda: (K.gemm_tn(v_o1, a1s, g("attn1.A_o")), K.gemm_tn(dh1, uo1, g("attn1.B_o"), st.scale)),
+            rt.side.launch(lambda: (rt.dw(v_o1, a1s, g("attn1.A_o")), rt.dw(dh1, uo1, g("attn1.B_o"), st.scale)),
                            v_o1, a1s, dh1, uo1)
         else:
             da1 = K.gemm(dh1, o1.wt)
@@ -595,13 +598,13 @@ class BasicTransformerBlock(nn.Module):
             n1s, u_qkv = sv["n1"], sv["u_qkv"]
 
             def dw_attn1():
-                K.gemm_tn(v_qkv, n1s, g("attn1.A_qkv"))
+                rt.dw(v_qkv, n1s, g("attn1.A_qkv"))
                 gB = g("attn1.B_qkv")
                 if r in K.TN_RANKS:
-                    K.gemm_tn(dqkv, u_qkv, gB, st.scale, group=C)
+                    rt.dw(dqkv, u_qkv, gB, st.scale, group=C)
                 else:
                     for j in range(3):
-                        K.gemm_tn(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
+                        rt.dw(dqkv[:, j * C:(j + 1) * C], u_qkv[:, j * r:(j + 1) * r], gB[j * C:(j + 1) * C],
                                   st.scale)
             rt.side.launch(dw_attn1, v_qkv, n1s, dqkv, u_qkv)
         else:
@@ -1266,7 +1269,17 @@ class UNet2DConditionModel(nn.Module):
                                   accumulate=True)
         else:
             dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True)
-        done = getattr(rt, "unit_done", None) or (lambda unit: None)  # overlapped gradient sync (trainer.GradBuckets)
+        unit_done = getattr(rt, "unit_done", None) or (lambda unit: None)  # overlapped gradient sync (GradBuckets)
+        # LoRA weight gradients are deferred per gradient unit and issued as one batched launch per rank / orientation
+        # (K.TnRankQueue) right before the unit is reported done -- its all-reduce bucket may be issued next
+        dwq = K.TnRankQueue() if TN_BATCH else None
+        rt.dw = dwq.add if dwq is not None else K.gemm_tn
+
+        def done(unit):
+            if dwq is not None:
+                dwq.flush()
+            unit_done(unit)
+
         done("conv_out")
         skip_grads = []
         for i in reversed(range(len(self.up_blocks))):
@@ -1319,6 +1332,8 @@ class UNet2DConditionModel(nn.Module):
             self._embed_bwd(fg, rt)
             done("embed")
         rt.saved.clear()  # activations of the never-differentiated prefix
+        if dwq is not None:
+            dwq.flush()
         rt.side.join()  # LoRA weight gradients complete before anything reads lora.grad
         return None
 

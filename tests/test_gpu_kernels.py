@@ -420,3 +420,37 @@ def test_fullgrad_helpers(cuda):
         Ct = C1 + C2
         u = u.view(B, Ct, 9, -1).permute(0, 3, 2, 1).reshape(-1, 9 * Ct)  # -> (pixel, tap, c)
         assert cols.shape == u.shape and torch.equal(cols.float(), u), (mode, stride, C1, C2)
+
+
+def test_tn_rank_batch_equals_individual_products(cuda):
+    """pso_gemm_tn_rank_batch (TnRankQueue: the deferred LoRA dA / dB products of a gradient unit in one launch per
+    rank / orientation) against the same products issued one by one, and against fp32 torch: mixed M (ragged last
+    row step included), C, ranks 32 / 64 / 96, the grouped q/k/v form and both orientations, accumulated twice."""
+    from pairwise_sample_optimization_amd import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(21)
+    specs = [  # (M, I, J, group) for gemm_tn(a [M, I], b [M, J]) -> out [I, r]
+        (8192, 1280, 32, 0), (8192, 32, 1280, 0), (4000, 640, 32, 0), (8192, 96, 1280, 0),
+        (8192, 3840, 96, 1280), (616, 64, 2048, 0), (616, 2560, 64, 1280), (33, 256, 32, 0), (32768, 640, 32, 0)]
+    ops = []
+    for M, I, J, grp in specs:
+        a = torch.randn(M, I, device=cuda, generator=g).bfloat16()
+        b = torch.randn(M, J, device=cuda, generator=g).bfloat16()
+        r = J * grp // I if grp else J
+        ops.append((a, b, grp, torch.zeros(I, r, device=cuda), torch.zeros(I, r, device=cuda)))
+    q = K.TnRankQueue()
+    for rep in range(2):
+        for a, b, grp, o1, o2 in ops:
+            K.gemm_tn(a, b, o1, 0.5, group=grp)
+            q.add(a, b, o2, 0.5, group=grp)
+        q.flush()
+    torch.cuda.synchronize()
+    for (M, I, J, grp), (a, b, _, o1, o2) in zip(specs, ops):
+        if grp:
+            r = J * grp // I
+            ref = torch.cat([a[:, j * grp:(j + 1) * grp].float().t() @ b[:, (j * grp // grp) * r:(j + 1) * r].float()
+                             for j in range(I // grp)], 0)
+        else:
+            ref = a.float().t() @ b.float()
+        ref = ref * 1.0  # two accumulations of alpha 0.5
+        assert ((o2 - o1).norm() / o1.norm()).item() < 1e-5, (M, I, J, grp)
+        assert ((o2 - ref).norm() / ref.norm()).item() < 1e-3, (M, I, J, grp)

@@ -17,7 +17,7 @@ for r in $(seq 1 $rounds); do
       env) envs="${a//,/ }" ;;
       tree) [ $a = prev ] && D=$PWD/ab/prev ;;
     esac
-    (cd $D && env $envs timeout -k 10 400 python -u bench.py --steps ${STEPS:-8} --warmup 3 --no-cpu-baseline --no-roofline) \
+    (cd $D && env $envs timeout -k 10 400 python -u bench.py --steps ${STEPS:-8} --warmup 3 --no-cpu-baseline --no-roofline --no-extra --epochs 0) \
         > "gpurun_out/ab_${kind}_$a.json" 2> "gpurun_out/ab_${kind}_$a.err" || { tail -5 "gpurun_out/ab_${kind}_$a.err"; exit 1; }
     echo "$kind $a round $r: $(python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['value'],'imgs/s',d['ms_per_step'],'ms')" "gpurun_out/ab_${kind}_$a.json")"
   done

@@ -7,7 +7,7 @@ T=${1:-prof}
 mkdir -p gpurun_out
 rm -rf gpurun_out/${T}_trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_trace -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --epochs 0 ${BENCH_ARGS:-} > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --epochs 0 --no-extra ${BENCH_ARGS:-} > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
     || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
 cat gpurun_out/${T}_bench.json
 python3 tools/step_breakdown.py $(find gpurun_out/${T}_trace -name '*kernel_trace.csv' | head -1) \
