@@ -3,8 +3,9 @@
 Workload (BASELINE.json configs[1]): SDXL-Turbo PSO, bf16, 1024x1024 (128x128 latents), 2-step
 sampler (T = 1 trained transition; a literal 1-step sampler trains nothing), LoRA r=32 grads only,
 2 pairs per micro-step per GPU, gradient_accumulation_steps 2 (the turbo config default).  One bench "step" = one
-optimizer step = gas*T micro-steps (+ the per-inner-epoch buffer shuffle, RCCL all-reduce, clip, AdamW); each
-micro-step trains 2P images (2P policy UNet fwd+bwd + 2P reference fwd + fused loss).  Synthetic data: random-init
+optimizer step = gas*T micro-steps (+ the per-inner-epoch buffer shuffle, RCCL all-reduce, clip, and the 8-bit
+AdamW of the reference default config -- --adam32 for fp32 AdamW); each micro-step trains 2P images (2P policy UNet
+fwd+bwd + 2P reference fwd + fused loss).  Synthetic data: random-init
 SDXL weights (seeded), N(0,1) text embeddings, trajectories from this build's own sampler (untimed), U(0,1)
 rewards.  Multi-GPU: one process per GPU, pure data parallel (weak scaling); the LoRA gradient is all-reduced over RCCL in
 ~32 MB buckets issued during the backward of the window's last micro-step (GradBuckets), overlapped with it.
@@ -65,6 +66,8 @@ def parse():
     ap.add_argument("--full-unet", action="store_true",
                     help="train every UNet parameter against a frozen reference UNet (BASELINE C3 / C4; use with "
                          "--mode dmd --num-steps 4 --pairs 1 --gas 1)")
+    ap.add_argument("--adam32", action="store_true",
+                    help="fp32 AdamW instead of the reference default 8-bit AdamW (config use_8bit_adam = True)")
     ap.add_argument("--allreduce-bf16", action="store_true",
                     help="bf16 gradient all-reduce (fp32 accumulation and optimizer; half the xGMI bytes)")
     ap.add_argument("--no-extra", action="store_true", help="skip the c3 / lora_bs1 secondary objects")
@@ -98,7 +101,8 @@ def build(args, dev):
     unet.prepare()
     tr = PSOTrainer(unet, mode=args.mode, num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
                     train_batch_size=args.pairs, num_reward=1, ref_unet=ref_unet,
-                    allreduce_dtype=torch.bfloat16 if getattr(args, "allreduce_bf16", False) else None)
+                    allreduce_dtype=torch.bfloat16 if getattr(args, "allreduce_bf16", False) else None,
+                    use_8bit_adam=not getattr(args, "adam32", False))  # the reference default (T:427-435)
     g = torch.Generator(device=dev).manual_seed(1000 + int(os.environ.get("RANK", "0")))
     Bp = args.pairs * args.gas  # pairs sampled per epoch per GPU
     enc = torch.randn(Bp, 77, 2048, device=dev, generator=g).bfloat16()

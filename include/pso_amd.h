@@ -355,6 +355,18 @@ int pso_grad_clip_coef(long n, const float* grad, float grad_scale, float max_no
 int pso_adamw_step(long n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
                    float beta2, float eps, float weight_decay, int step, float grad_scale, const float* clip_coef,
                    void* stream);
+/* Blockwise 8-bit AdamW (bitsandbytes AdamW8bit, the reference's default optimizer: config_sdxl_turbo_dpo.py:86
+ * `use_8bit_adam = True`, T:427-435).  exp_avg_q / exp_avg_sq_q are uint8 codes [n] into the signed / unsigned dynamic
+ * quantisation maps (pso_adamw8bit_maps), absmax_m / absmax_v one fp32 scale per 2048-element block
+ * (pso_adamw8bit_blocks(n) of each); all zero-initialised.  Per element: dequantise with the block's previous absmax,
+ * m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p += -lr c2/c1 * m / (sqrt(v) + c2 eps), p *= 1 - lr wd (c1 = 1-b1^t,
+ * c2 = sqrt(1-b2^t)), then requantise to the nearest code against the block's new absmax.  g = grad * grad_scale *
+ * clip_coef[1] (clip_coef may be NULL).  Parity unpinned (bitsandbytes is not in this image; oracle/adam8bit.py). */
+size_t pso_adamw8bit_blocks(long n);
+void pso_adamw8bit_maps(float* signed_map, float* unsigned_map);
+int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
+                       float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream);
 int pso_zero_f32(long n, float* x, void* stream);
 int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
                    void* stream);

@@ -108,6 +108,9 @@ SIGNATURES = {
     "pso_gather_rows": (ci, [cl, cl, vp, vp, vp, vp]),
     "pso_grad_clip_coef": (ci, [cl, vp, cf, cf, vp, vp, csz, vp]),
     "pso_adamw_step": (ci, [cl, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
+    "pso_adamw8bit_blocks": (csz, [cl]),
+    "pso_adamw8bit_maps": (None, [vp, vp]),
+    "pso_adamw8bit_step": (ci, [cl, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
     "pso_zero_f32": (ci, [cl, vp, vp]),
     "pso_preference": (ci, [ci, ci, vp, vp, ci, vp, vp]),
     "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),

@@ -788,7 +788,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
-  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39) ? 0 : gv_raw;
+  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40) ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
@@ -847,18 +847,24 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // vs 770); at K = 640 / 1280 the 2-phase 128 x 160 with two co-resident blocks per CU (one block's epilogue beside
   // the other's main loop) stays ahead (16384 x 1280 x 1280 827 vs 724, tools/shape_prof.py one box).  Variant 37
   // keeps the 2-phase 128 x 160, 38 forces the 8-phase form wherever it applies.
+  // 8-phase 256 x 320 (gemm8p.hip): every SDXL width is a multiple of 320, and at the UNet's M (256 * 2^k rows) the
+  // tile count is a whole number of 256-CU rounds (N = 1280 at M = 16384: 256 tiles; N = 640 at M = 65536: 512).
+  // Default where it fills at least one round and the reduction is short (K < 2560: the 256 x 160 persistent form
+  // keeps the long ones); at half a round (M = 8192, N = 1280: 128 tiles) the 2-phase 128 x 160 stays ahead
+  // (tools/shape_prof.py, one box: 16384 x 1280 x 1280 + LoRA 922 vs 816 TF/s, 65536 x 640 x 640 + LoRA 700 vs 652,
+  // 65536 x 1920 x 640 + LoRA 849 vs 783; 8192 x 1280 x 1280 + LoRA 574 vs 776).  Variant 39 forces it, 40 keeps it
+  // off.
+  const bool ok320 = base8 && (g.N % 320) == 0 && g.lda1 == g.ldb1 && (!g.a2 || g.K2 <= 64) &&
+                     (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
+  const long t320 = (long)((g.M + 255) / 256) * (g.N / 320);
+  if (ok320 && gv_raw != 40 && (gv_raw == 39 || (gv == 0 && t320 >= 256 && Ktot < 2560 && g.N < 2560)))
+    return pso_gemm8p320_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
+                             g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   const bool ok160 = base8 && (g.N % 160) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
   const long t160 = (long)((g.M + 255) / 256) * (g.N / 160);
   if (ok160 && gv_raw != 37 && (gv_raw == 38 || (gv == 0 && t160 >= 256 && Ktot >= 2560)))
     return pso_gemm8p160_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
-  // 8-phase 256 x 320 (gemm8p.hip): every SDXL width is a multiple of 320, and at the UNet's M (256 * 2^k rows) the
-  // tile count is a whole number of 256-CU rounds (N = 1280 at M = 16384: 256 tiles; N = 640 at M = 65536: 512).
-  // Variant 39 forces it where it applies (A/B knob).
-  const bool ok320 = base8 && (g.N % 320) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
-  if (ok320 && gv_raw == 39) return pso_gemm8p320_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2,
-                                                      g.b2, g.ldb2, g.tail_m, g.tail_group_n, g.alpha, g.bias, g.resid,
-                                                      g.ldr, g.out, g.ldo, g.group_m, st);
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);

@@ -142,8 +142,12 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   }
   const int m0 = bm * 256, n0 = bn * BN;
   const int nt1 = g.K / KT;  // K % KT == 0 (host-checked)
-  // the LoRA K-tail: tiles made only of rows >= tail_m (the reference half of a paired pass) skip it (zero there)
-  const int nt2 = (g.a2 && m0 < g.tail_m) ? (g.K2 + KT - 1) / KT : 0;
+  // the LoRA K-tail: tiles made only of rows >= tail_m (the reference half of a paired pass) skip it (zero there).
+  // RT (256 x 320): the tail is NOT staged through the ring -- it runs after the main loop from register operands
+  // (register budget: the tail's per-lane staging addresses inside the 8-phase loop spill the 160 accumulators)
+  constexpr bool RT = BN == 320;
+  const bool has_tail = g.a2 && m0 < g.tail_m;
+  const int nt2 = (!RT && has_tail) ? (g.K2 + KT - 1) / KT : 0;
   const int nt = (nt1 + nt2 + 1) & ~1;  // the 8-phase loop consumes K-tiles in pairs: an odd count gets a zero tile
 
   // staging: wave w fills pieces 2w, 2w+1 (8 rows x 128 B each) of every half-tile image; the XOR swizzle is applied
@@ -157,7 +161,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // base, the half and the K-tile advance are wave-uniform and go in the scalar soffset.  Rows past M read as zeros
   // through rA's range (they are never stored), so no per-lane clamp is needed.
   const unsigned vA = (unsigned)(prow * (int)g.lda * ES + (pch ^ prow) * 16);
-  const unsigned vW = (unsigned)(prow * (int)g.ldw * ES + (pch ^ prow) * 16);
+  // (256 x 320: the host guarantees lda == ldw, and A's register serves both operands)
+  const unsigned vW = BN == 320 ? vA : (unsigned)(prow * (int)g.ldw * ES + (pch ^ prow) * 16);
   // row (inside its image) of this lane in B piece i of this wave (LoRA tail path)
   auto bpiece_row = [&](int i) { return (i < 2 ? wave * 2 + i : 16 + wave) * 8 + prow; };
   const __amdgpu_buffer_rsrc_t rA =
@@ -175,9 +180,12 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     const int half = img & 3;
     bf16_t* dst = l8 + img_off(img) + wave * 2 * 8 * 64;
     if (BN == 160 && half >= 2 && wave >= (half == 2 ? BW0 : BW1)) return;  // 96 / 64-row B images: waves 0-5 / 0-3
-    // the extra (third) B piece of waves 0-3 in the 256 x 320 form: piece 16 + w of the image
-    bf16_t* dst_x = l8 + img_off(img) + (16 + wave) * 8 * 64;
-    const bool xp = XP && half >= 2 && wave < 4;
+    // the extra (third) B piece in the 256 x 320 form: piece 16 + w of the image for waves 0-3; waves 4-7 issue the
+    // same load with a source past the buffer range (zeros, no memory traffic) into a dummy 1-KB slot behind the
+    // ring, so every wave issues 3 pieces per B image: no per-wave branch, one vmcnt count for all waves
+    bf16_t* dst_x = wave < 4 ? l8 + img_off(img) + (16 + wave) * 8 * 64 : l8 + 4 * HT + 4 * (BN / 2) * 64 + (wave - 4) * 512;
+    const bool xp = XP && half >= 2;
+    const int xsrc_oob = wave < 4 ? 0 : (int)OOB;  // in the scalar soffset: no extra lane register
     if (kt < nt1) {
       const int k0 = kt * 128;  // bytes
       if (half < 2) {
@@ -190,10 +198,14 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, vW, sw + 8 * (int)g.ldw * ES, 0,
                                                  0);
         if constexpr (XP)
-          if (xp)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rW, (lds8_void*)dst_x, 16, vW, (n0 + (half & 1) * BH0 + (16 + wave) * 8) * (int)g.ldw * ES + k0, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rW, (lds8_void*)dst_x, 16, vW, ((n0 + (half & 1) * BH0 + (16 + wave) * 8) * (int)g.ldw * ES + k0) | xsrc_oob,
+              0, 0);
       }
+    } else if constexpr (RT) {  // the zero pad tile of an odd K-tile count: every load past the buffer range
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, OOB, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, OOB, 0, 0, 0);
+      if (xp) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst_x, 16, OOB, 0, 0, 0);
     } else {  // LoRA K-tail (one or two K-tiles per output tile) or the zero pad tile
       const int kc = (kt - nt1) * KT + (pch ^ prow) * (16 / ES);  // this lane's 16-B chunk of the tail
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
@@ -355,9 +367,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // the counted wait that retires all but the last three stagings (B0, A1, B1): 6 loads per wave, fewer for the waves
   // that stage no B1 (4) or no B pieces at all (2) in the 256 x 160 form
   auto vm_wait6 = [&]() {
-    if constexpr (BN == 320) {  // waves 0-3 stage 3 pieces per B image: 3 + 2 + 3 in flight, the others 2 + 2 + 2
-      if (wave < 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if constexpr (BN == 320) {  // every wave stages 3 pieces per B image (see stage): 3 + 2 + 3 in flight
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       if (BN == 256 || wave < BW1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else if (wave < BW0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -407,6 +418,44 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   }
 #undef PHASE
   // FP8: the inline-asm MFMAs are invisible to the hazard recognizer -- pad before any VALU reads an accumulator
+  if constexpr (RT) {
+    // LoRA K-tail from register operands (K2 <= 64 in steps of 32 = one MFMA k-depth): this lane's fragments are
+    // 16-B global loads -- A2 row m0 + 128 ha + 32 wr + 16 i + fr and W2 row n0 + hb*BH0 + wc*CW0 + 16 j + fr, k =
+    // kb + 8 fk .. +8 -- u / sB are small and L2-resident.  Rows >= tail_m (the reference half of a paired pass)
+    // and k >= K2 are zeros.
+    if (has_tail) {
+      const bf16x8 z8 = __builtin_bit_cast(bf16x8, make_uint4(0u, 0u, 0u, 0u));
+      for (int kb = 0; kb < g.K2; kb += 32) {
+        const int k = kb + 8 * fk;
+        bf16x8 ta2[2][MI], tw2[2][NJ];
+#pragma unroll
+        for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int m = m0 + ha * 128 + wr * 32 + i * 16 + fr;
+            ta2[ha][i] = (m < g.tail_m && k < g.K2)
+                             ? *reinterpret_cast<const bf16x8*>(g.a2 + (long)m * g.lda2 + a2_col + k) : z8;
+          }
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + hb * BH0 + wc * CW0 + j * 16 + fr;
+            tw2[hb][j] = k < g.K2 ? *reinterpret_cast<const bf16x8*>(g.w2 + (long)n * g.ldw2 + k) : z8;
+          }
+#pragma unroll
+        for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+          for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[ha][hb][i][j]) : "v"(tw2[hb][j]),
+                             "v"(ta2[ha][i]));
+      }
+    }
+  }
   if constexpr (FP8 || BN == 320) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   if (STAG && wave < 4) __builtin_amdgcn_s_barrier();
   if (SPRIO) __builtin_amdgcn_s_setprio(0);
@@ -691,7 +740,8 @@ static const int g_grid8 = [] {
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
 int launch8(const Gemm8Args& g, hipStream_t st) {
   const int nblk = ((g.M + 255) / 256) * (g.N / BN);
-  const size_t shm = (4 * HT + 4 * (BN / 2) * 64) * sizeof(bf16_t);  // 2 K-tile buffers: 128 KiB (256 x 256) / 104 KiB (256 x 160)
+  // 2 K-tile buffers: 128 KiB (256 x 256) / 104 KiB (256 x 160) / 144 KiB + a 4-KiB dummy slot (256 x 320)
+  const size_t shm = (4 * HT + 4 * (BN / 2) * 64 + (BN == 320 ? 4 * 512 : 0)) * sizeof(bf16_t);
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN>,

@@ -10,6 +10,10 @@
 //                      compare D:420-434 (strict Pareto dominance, ties -> (0, 0)).
 #include "common.h"
 
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 #define OPT_THREADS 256
 
 // partial sums of g^2 (fp64) per block -> one final block computes the clip coefficient
@@ -70,6 +74,112 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
     pi -= step * (mi / denom);
     p[i] = pi;
   }
+}
+
+// ---- blockwise 8-bit AdamW (bitsandbytes AdamW8bit: the reference default, config_sdxl_turbo_dpo.py:86, T:427-435)
+// m and v live as uint8 codes into two 256-entry dynamic quantisation maps (signed for m, unsigned for v) with one
+// fp32 absmax per 2048-element block; each step dequantises with the previous absmax, updates, and requantises
+// (nearest code) against the block's new absmax.  One 256-thread workgroup per block, 8 consecutive elements per
+// thread; the maps travel in the kernel arguments and sit in LDS.  Arithmetic in the order of bitsandbytes'
+// kOptimizerStatic8bit2StateBlockwise ADAM branch (restated in oracle/adam8bit.py, parity unpinned: no bitsandbytes
+// here), contraction off so the fp32 rounding matches the restatement step for step.
+#define ADAM8_BLOCK 2048
+struct Adam8Maps {
+  float s[256], u[256];
+};
+
+__device__ __forceinline__ int adam8_nearest(const float* __restrict__ code, float x) {
+  // lower_bound over the sorted map, then the nearer of the two neighbours (ties -> the lower index)
+  int lo = 0, n = 256;
+  while (n > 0) {
+    const int h = n >> 1;
+    if (code[lo + h] < x) { lo += h + 1; n -= h + 1; }
+    else n = h;
+  }
+  int idx = lo < 1 ? 1 : (lo > 255 ? 255 : lo);
+  const float a = code[idx - 1], b = code[idx];
+  return fabsf(x - a) <= fabsf(b - x) ? idx - 1 : idx;
+}
+
+__global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                        uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
+                                                        float* __restrict__ am, float* __restrict__ av, float b1,
+                                                        float omb1, float b2, float omb2, float eps_c2, float step_size,
+                                                        float decay, float gscale, const float* __restrict__ clip,
+                                                        Adam8Maps maps) {
+#pragma clang fp contract(off)
+  __shared__ float cs[256], cu[256];
+  __shared__ float red[2][4];
+  const int t = threadIdx.x;
+  cs[t] = maps.s[t];
+  cu[t] = maps.u[t];
+  const long blk = blockIdx.x;
+  const long i0 = blk * ADAM8_BLOCK + (long)t * 8;
+  const float s = gscale * (clip ? clip[1] : 1.0f);
+  const float am0 = am[blk], av0 = av[blk];
+  __syncthreads();
+  float m[8], v[8], pv[8];
+  float mx_m = 0.f, mx_v = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long i = i0 + e;
+    if (i < n) {
+      const float gi = g[i] * s;
+      m[e] = cs[qm[i]] * am0;
+      v[e] = cu[qv[i]] * av0;
+      m[e] = (m[e] * b1) + (omb1 * gi);
+      v[e] = (v[e] * b2) + ((omb2 * gi) * gi);
+      pv[e] = p[i] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
+      pv[e] = pv[e] * decay;
+      mx_m = fmaxf(mx_m, fabsf(m[e]));
+      mx_v = fmaxf(mx_v, fabsf(v[e]));
+    } else {
+      m[e] = v[e] = pv[e] = 0.f;
+    }
+  }
+  // block maxima: wave (64 lanes) then the 4 waves
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx_m = fmaxf(mx_m, __shfl_xor(mx_m, o, 64));
+    mx_v = fmaxf(mx_v, __shfl_xor(mx_v, o, 64));
+  }
+  if ((t & 63) == 0) { red[0][t >> 6] = mx_m; red[1][t >> 6] = mx_v; }
+  __syncthreads();
+  const float nm = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  const float nv = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const long i = i0 + e;
+    if (i >= n) continue;
+    p[i] = pv[e];
+    qm[i] = (uint8_t)adam8_nearest(cs, nm > 0.f ? m[e] / nm : 0.f);
+    qv[i] = (uint8_t)adam8_nearest(cu, nv > 0.f ? v[e] / nv : 0.f);
+  }
+  if (t == 0) { am[blk] = nm; av[blk] = nv; }
+}
+
+// bitsandbytes.functional.create_dynamic_map(signed, max_exponent_bits = 7, total_bits = 8), float32 like the
+// torch original (numpy-style linspace in double, cast to float32)
+static void adam8_dynamic_map(bool sgn, float* out) {
+  std::vector<float> d;
+  const int max_exp = 7, non_sign = 7;
+  for (int i = 0; i < max_exp; ++i) {
+    const int nitems = sgn ? (1 << (i + non_sign - max_exp)) + 1 : (1 << (i + non_sign - max_exp + 1)) + 1;
+    std::vector<float> b(nitems);
+    const double step = (1.0 - 0.1) / (nitems - 1);
+    for (int k = 0; k < nitems; ++k) b[k] = (float)(k == nitems - 1 ? 1.0 : 0.1 + k * step);
+    const float sc = (float)std::pow(10.0, (double)(-(max_exp - 1) + i));
+    for (int k = 0; k + 1 < nitems; ++k) {
+      const float mean = (b[k] + b[k + 1]) / 2.0f;
+      d.push_back(sc * mean);
+      if (sgn) d.push_back(-sc * mean);
+    }
+  }
+  d.push_back(0.f);
+  d.push_back(1.f);
+  while (d.size() < 256) d.push_back(0.f);
+  std::sort(d.begin(), d.end());
+  for (int k = 0; k < 256; ++k) out[k] = d[k];
 }
 
 __global__ void zero_kernel(long n, float* __restrict__ x) {
@@ -133,6 +243,36 @@ int pso_adamw_step(long n, float* param, const float* grad, float* exp_avg, floa
                                                                     beta2, eps, weight_decay, bc1, sqrtf(bc2),
                                                                     grad_scale, clip_coef);
   return pso_check_launch("pso_adamw_step");
+}
+
+size_t pso_adamw8bit_blocks(long n) { return (size_t)((n + ADAM8_BLOCK - 1) / ADAM8_BLOCK); }
+
+void pso_adamw8bit_maps(float* signed_map, float* unsigned_map) {
+  adam8_dynamic_map(true, signed_map);
+  adam8_dynamic_map(false, unsigned_map);
+}
+
+int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
+                       float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
+  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0,
+                "pso_adamw8bit_step: bad args");
+  static Adam8Maps maps = [] {
+    Adam8Maps m;
+    adam8_dynamic_map(true, m.s);
+    adam8_dynamic_map(false, m.u);
+    return m;
+  }();
+  const double b1 = beta1, b2 = beta2;
+  const float c1 = (float)(1.0 - std::pow(b1, step));
+  const float c2 = (float)std::sqrt(1.0 - std::pow(b2, step));
+  const float step_size = (-lr) * c2 / c1;
+  const float decay = (float)(1.0 - (double)lr * weight_decay);
+  const int nb = (int)pso_adamw8bit_blocks(n);
+  adamw8bit_kernel<<<nb, 256, 0, (hipStream_t)stream>>>(n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v,
+                                                         beta1, (float)(1.0 - b1), beta2, (float)(1.0 - b2),
+                                                         c2 * eps, step_size, decay, grad_scale, clip_coef, maps);
+  return pso_check_launch("pso_adamw8bit_step");
 }
 
 int pso_zero_f32(long n, float* x, void* stream) {

@@ -727,6 +727,37 @@ def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, s
                                float(grad_scale), ptr(clip), stream_ptr()), "pso_adamw_step")
 
 
+class Adam8State:
+    """State of the blockwise 8-bit AdamW (bitsandbytes AdamW8bit) for a flat fp32 parameter of n elements: uint8
+    codes of m and v, one fp32 absmax per 2048-element block of each; zero-initialised like bitsandbytes."""
+
+    def __init__(self, n, device):
+        nb = lib().pso_adamw8bit_blocks(n)
+        self.qm = torch.zeros(n, dtype=torch.uint8, device=device)
+        self.qv = torch.zeros(n, dtype=torch.uint8, device=device)
+        self.am = torch.zeros(nb, dtype=torch.float32, device=device)
+        self.av = torch.zeros(nb, dtype=torch.float32, device=device)
+
+    def dequant(self):
+        """(m, v) as fp32 (tests / checkpoints)."""
+        s = (ctypes.c_float * 256)()
+        u = (ctypes.c_float * 256)()
+        lib().pso_adamw8bit_maps(s, u)
+        cs = torch.tensor(list(s), device=self.qm.device)
+        cu = torch.tensor(list(u), device=self.qm.device)
+        n = self.qm.numel()
+        blk = torch.arange(n, device=self.qm.device) // 2048
+        return cs[self.qm.long()] * self.am[blk], cu[self.qv.long()] * self.av[blk]
+
+
+def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None):
+    require_cuda(param, grad)
+    check(lib().pso_adamw8bit_step(param.numel(), ptr(param), ptr(grad), ptr(state.qm), ptr(state.qv), ptr(state.am),
+                                   ptr(state.av), float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                   float(weight_decay), int(step), float(grad_scale), ptr(clip), stream_ptr()),
+          "pso_adamw8bit_step")
+
+
 def zero_(x):
     check(lib().pso_zero_f32(x.numel(), ptr(x), stream_ptr()), "pso_zero_f32")
     return x

@@ -66,8 +66,12 @@ def load_lora_into_unet(state_dict, network_alphas, unet):
 def save_state(trainer, output_dir):
     unet = trainer.unet
     save_lora_weights(output_dir, peft_to_diffusers(get_peft_model_state_dict(unet)))
-    save_file({"exp_avg": trainer.exp_avg.cpu(), "exp_avg_sq": trainer.exp_avg_sq.cpu()},
-              os.path.join(output_dir, OPT_NAME),
+    a8 = getattr(trainer, "adam8", None)
+    if a8 is not None:  # 8-bit AdamW state as it stands (codes + block absmax): a resume continues bit for bit
+        opt = {"exp_avg_q": a8.qm.cpu(), "exp_avg_sq_q": a8.qv.cpu(), "absmax_m": a8.am.cpu(), "absmax_v": a8.av.cpu()}
+    else:
+        opt = {"exp_avg": trainer.exp_avg.cpu(), "exp_avg_sq": trainer.exp_avg_sq.cpu()}
+    save_file(opt, os.path.join(output_dir, OPT_NAME),
               metadata={"step": str(trainer.opt_step), "n_micro": str(trainer.n_micro)})
     with open(os.path.join(output_dir, "pso_state.json"), "w") as f:
         json.dump({"opt_step": trainer.opt_step, "n_micro": trainer.n_micro, "rank": unet.lora.r}, f)
@@ -77,8 +81,17 @@ def load_state(trainer, input_dir):
     sd, alphas = lora_state_dict(input_dir)
     load_lora_into_unet(sd, alphas, trainer.unet)
     opt = load_file(os.path.join(input_dir, OPT_NAME))
-    trainer.exp_avg.copy_(opt["exp_avg"])
-    trainer.exp_avg_sq.copy_(opt["exp_avg_sq"])
+    a8 = getattr(trainer, "adam8", None)
+    if a8 is not None:
+        if "exp_avg_q" not in opt:
+            raise KeyError("checkpoint holds fp32 AdamW state; this trainer runs the 8-bit AdamW (use_8bit_adam)")
+        for t, k in ((a8.qm, "exp_avg_q"), (a8.qv, "exp_avg_sq_q"), (a8.am, "absmax_m"), (a8.av, "absmax_v")):
+            t.copy_(opt[k])
+    else:
+        if "exp_avg" not in opt:
+            raise KeyError("checkpoint holds 8-bit AdamW state; this trainer runs fp32 AdamW")
+        trainer.exp_avg.copy_(opt["exp_avg"])
+        trainer.exp_avg_sq.copy_(opt["exp_avg_sq"])
     with open(os.path.join(input_dir, "pso_state.json")) as f:
         meta = json.load(f)
     trainer.opt_step, trainer.n_micro = int(meta["opt_step"]), int(meta["n_micro"])

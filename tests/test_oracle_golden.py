@@ -81,3 +81,19 @@ def test_compare_rules():
     np.testing.assert_array_equal(pm.sample_compare(a, b, np.zeros(3, int)), [[-1, 1], [1, -1], [-1, 1]])
     # dmd: strict pareto, ties -> (0, 0)
     np.testing.assert_array_equal(pm.compare(a, b), [[-1, 1], [1, -1], [0, 0]])
+
+
+def test_adam8bit_dynamic_maps():
+    """bitsandbytes' dynamic quantisation maps (oracle/adam8bit.py): 256 sorted codes, signed map symmetric with one
+    zero and 1.0 at the top, unsigned map on [0, 1]."""
+    import numpy as np
+    from oracle.adam8bit import create_dynamic_map, quantize_nearest
+    s, u = create_dynamic_map(True), create_dynamic_map(False)
+    assert s.shape == (256,) and u.shape == (256,)
+    assert (np.diff(s) >= 0).all() and (np.diff(u) >= 0).all()
+    assert s[-1] == 1.0 and u[-1] == 1.0 and u[0] == 0.0 and (u >= 0).all()
+    assert (s == 0).sum() == 1 and np.allclose(np.sort(-s[s < 0]), np.sort(s[(s > 0) & (s < 1)]))
+    assert s.min() > -1.0 and abs(s[s > 0].min() - 5.5e-7) < 1e-7
+    x = np.array([0.0, 1.0, -0.3, 0.31, 1e-7], dtype=np.float32)
+    q = quantize_nearest(x, s)
+    assert s[q[0]] == 0.0 and s[q[1]] == 1.0 and abs(s[q[2]] + 0.3) < 0.02 and abs(s[q[3]] - 0.31) < 0.02
