@@ -179,9 +179,14 @@ def test_graph_epoch_equals_eager_epoch_fp8(cuda):
     le, lg, le2 = (torch.stack(t.loss_hist).cpu() for t in (tr_e, tr_g, tr_e2))
     assert torch.equal(le[0], lg[0]), (le, lg)  # before any update: same kernels, same inputs, same bits
     assert (le - 0.6931471805599453).abs().max() > 1e-3, "the LoRA must move the loss (not clipped, not zero)"
-    spread = (le - le2).abs()
-    bar = torch.maximum(3 * spread, 2e-3 * le.abs()) + 1e-5
-    print(f"fp8 graph-vs-eager losses {lg.tolist()} vs {le.tolist()}, eager spread {spread.tolist()}")
+    # the eager run-to-run spread (split-K f32 atomics in the weight gradients, amplified by beta) is measured on each
+    # epoch and the largest relative one bounds every epoch: one epoch's spread alone can land far below the typical
+    # one by chance.  A replay of capture-time fp8 copies misses every update -- losses that the eager run moves by
+    # ~8x over these epochs.
+    rel_spread = ((le - le2).abs() / le.abs()).max().item()
+    bar = max(3 * rel_spread, 1e-2) * le.abs() + 1e-5
+    print(f"fp8 graph-vs-eager losses {lg.tolist()} vs {le.tolist()}, eager rel spread {rel_spread:.3g}")
+    assert le[0] / le[1:].min() > 2, "the updates must move the loss well past the bar"
     assert ((le - lg).abs() <= bar).all(), (le, lg, le2)
     # the LoRA state moved: the fp8 copies the graph reads must have followed it
     assert (u_g.lora.master - u_e.lora.master).abs().max().item() <= \
