@@ -788,7 +788,8 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
-  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40) ? 0 : gv_raw;
+  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42)
+                     ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
@@ -857,7 +858,8 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const bool ok320 = base8 && (g.N % 320) == 0 && g.lda1 == g.ldb1 && (!g.a2 || g.K2 <= 64) &&
                      (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
   const long t320 = (long)((g.M + 255) / 256) * (g.N / 320);
-  if (ok320 && gv_raw != 40 && gv_raw != 38 && (gv_raw == 39 || (gv == 0 && t320 >= 256 && Ktot < 2560 && g.N < 2560)))
+  if (ok320 && gv_raw != 40 && gv_raw != 38 &&
+      (gv_raw == 39 || (gv == 0 && t320 >= 256 && g.N < 2560 && (gv_raw != 42 || Ktot < 2560))))
     return pso_gemm8p320_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   const bool ok160 = base8 && (g.N % 160) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);

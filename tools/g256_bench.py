@@ -37,6 +37,22 @@ def main():
         ms = t_ms(lambda: a @ w.t())
         res.append(f"hipBLASLt {fl / ms / 1e9:6.0f}")
         print(f"{M}x{N}x{Kd} [{kn}]: " + " | ".join(res) + " TF/s", flush=True)
+    # ff.out as the step runs it: bias + residual epilogue
+    M, N, Kd = 16384, 1280, 5120
+    a = torch.randn(M, Kd, device=dev).bfloat16()
+    w = torch.randn(N, Kd, device=dev).bfloat16()
+    b = torch.randn(N, device=dev).bfloat16()
+    r = torch.randn(M, N, device=dev).bfloat16()
+    fl = 2 * M * N * Kd
+    for v in variants:
+        K.lib().pso_gemm_set_variant(v)
+        res = []
+        for name, kw in (("plain", {}), ("bias", dict(bias=b)), ("bias+resid", dict(bias=b, resid=r))):
+            ms = t_ms(lambda: K.gemm(a, w, **kw))
+            res.append(f"{name} {fl / ms / 1e9:6.0f}")
+        print(f"ff.out {M}x{N}x{Kd} v{v} [{K.lib().pso_last_kernel().decode()}]: " + " | ".join(res) + " TF/s",
+              flush=True)
+    K.lib().pso_gemm_set_variant(0)
     # the GEGLU projection (fused epilogue, pre-activation saved for half the rows as in the paired pass)
     for M, N, Kd in [(16384, 10240, 1280), (65536, 5120, 640)]:
         a = torch.randn(M, Kd, device=dev).bfloat16()

@@ -27,16 +27,18 @@ def main():
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
     agg = defaultdict(lambda: [0, 0.0, 0.0])
-    for fl, nb, e0, e1, tag, _kname in rec:
+    kn = defaultdict(set)
+    for fl, nb, e0, e1, tag, kname in rec:
         a = agg[tag]
         a[0] += 1
         a[1] += e0.elapsed_time(e1)
         a[2] += fl
+        kn[tag].add(kname.replace("gemm8p_kernel", "8p").replace("gemm_bf16_kernel", "2p"))
     tot = sum(a[1] for a in agg.values())
     print(f"GEMM family: {len(rec)} launches, {tot:.1f} ms, {sum(a[2] for a in agg.values()) / tot / 1e9:.1f} TF/s")
     top = int(os.environ.get("SHAPE_TOP", "60"))
     for tag, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-        print(f"{ms:8.2f} ms {100 * ms / tot:5.1f}% n={n:4d} {fl / ms / 1e9:7.1f} TF/s  {tag}")
+        print(f"{ms:8.2f} ms {100 * ms / tot:5.1f}% n={n:4d} {fl / ms / 1e9:7.1f} TF/s  {tag}  {'/'.join(sorted(kn[tag]))}")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,7 @@
 """Per-kernel breakdown of the TIMED train steps inside a rocprofv3 kernel trace of bench.py.
-The window starts at the first GEMM-family dispatch of the last `steps * launches_per_step` family dispatches.
+The window runs from the end of the optimizer launch that closed the last warmup step to the end of the last step's
+optimizer launch (one AdamW launch per step); without steps + 1 of them, from the first GEMM-family dispatch of the
+last `steps * launches_per_step` family dispatches.
 usage: python tools/step_breakdown.py TRACE_CSV LAUNCHES_PER_STEP STEPS"""
 import csv
 import sys
@@ -20,9 +22,12 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    fam = [i for i, r in enumerate(rows) if any(k in r[2] for k in FAMILY)]
-    start = fam[-lps * steps]
-    win = rows[start:]
+    opt = [i for i, r in enumerate(rows) if "adamw" in r[2]]
+    if len(opt) >= steps + 1:
+        win = rows[opt[-steps - 1] + 1:opt[-1] + 1]
+    else:
+        fam = [i for i, r in enumerate(rows) if any(k in r[2] for k in FAMILY)]
+        win = rows[fam[-lps * steps]:]
     t0, t1 = win[0][0], max(r[1] for r in win)
     agg = defaultdict(lambda: [0, 0])
     for s, e, n in win:
