@@ -211,7 +211,11 @@ def test_c2_turbo_lora_window_at_1024(cuda):
     assert rp < 3e-2 and rr < 3e-2
     bar_d = 1.5 * rd16 + 2e-2
     bar_D = 1.5 * rD16 + 2e-2
-    bar_l = 1.5 * rel16 + 2e-3
+    # the loss is a function of the Deltas, and each Delta is dominated by |delta|^2 (c2^2 / 2 sigma^2 sum delta^2), so
+    # an uncorrelated bf16 error of ~11 % in delta (both runs above) biases every Delta by ~(0.11)^2 ~ 1 %: a loss
+    # floor of 5e-3 (the torch-bf16 run's own distance is a single draw: 1.6e-3 at b_std 6e-3, 6e-5 at 1.5e-2); the
+    # LoRA-off path sits at 2.7e-2 and is rejected below with a 2x margin
+    bar_l = 1.5 * rel16 + 5e-3
     assert rd <= bar_d and rd < 0.3
     assert rD <= bar_D and rD < 0.3
     assert rel <= bar_l
