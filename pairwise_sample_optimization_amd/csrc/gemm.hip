@@ -774,6 +774,9 @@ int pso_gemm8p160_run(int M, int N, int K, const void* a, long lda, const void* 
 int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2, long lda2,
                       int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha, const void* bias,
                       const void* resid, long ldr, void* out, long ldo, int group_m, hipStream_t st);
+int pso_gemm8p320_conv_run(int B, int H, int W, int C, const void* x, const void* w, int Cout, float alpha,
+                           const void* bias, const void* rowbias, long ld_rowbias, const void* resid, long ldr,
+                           void* out, long ldo, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 static int g_gemm_variant = 0;
@@ -788,7 +791,8 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
-  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42)
+  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
+                  gv_raw == 43 || gv_raw == 44)
                      ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
@@ -827,6 +831,23 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if (ks > ktiles / 2) ks = ktiles / 2;
     if (ks < 1) ks = 1;
     return launch<64, 64>(g, st, (int)ks);
+  }
+  // 3x3 / stride 1 / pad 1 convolutions (the ResNet convs and their input gradients) on the 8-phase 256 x 320 tiles
+  // (gemm8p.hip CONV form) wherever they fill a round of CUs; variant 43 keeps them on the 2-phase kernel, 44 forces it
+  {
+    const ConvGeom& cv = g.conv;
+    const long hw = (long)cv.Ho * cv.Wo;
+    const bool conv8 = cv.mode == PSO_CONV_NORMAL && cv.ks == 3 && cv.stride == 1 && cv.pad == 1 && cv.H == cv.Ho &&
+                       cv.W == cv.Wo && cv.C2 == 0 && (cv.C1 % 64) == 0 && cv.C1 <= 4096 && (hw % 256) == 0 &&
+                       (cv.H & (cv.H - 1)) == 0 && (cv.W & (cv.W - 1)) == 0 && cv.W >= 8 &&
+                       (g.N % 320) == 0 && !g.a2 && g.out_dtype == PSO_BF16 && !g.accumulate && al16(g.out) &&
+                       (g.ldo % 8) == 0 && (!g.resid || (al16(g.resid) && (g.ldr % 8) == 0)) &&
+                       (!g.bias || al8(g.bias)) && (!g.rowbias || (al8(g.rowbias) && g.rows_per_group == hw)) &&
+                       fits30((long)g.M + 2L * (cv.W + 1), cv.C1) && fits30(g.N, g.ldb1) && al16(g.a1) && al16(g.b1);
+    const long t320c = (long)(g.M / 256) * (g.N / 320);
+    if (conv8 && gv_raw != 43 && (gv_raw == 44 || (gv == 0 && t320c >= 256)))
+      return pso_gemm8p320_conv_run(g.M / (int)hw, cv.H, cv.W, cv.C1, g.a1, g.b1, g.N, g.alpha, g.bias, g.rowbias,
+                                    g.ld_rowbias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   }
   // 8-phase 256x256 (gemm8p.hip, wave groups staggered) for dense bf16 GEMMs with N % 256 == 0: LDS-staged 16-B
   // epilogue, LoRA K-tail, bias / alpha / residual.  Default for N >= 2560 with >= 256 tiles (tools/gemm8_ab.py, one

@@ -58,6 +58,10 @@ struct Gemm8Args {
   int skip_epi;  // benchmark knob: accumulators kept live, nothing stored (main-loop time alone)
   // FP8 form: E8M0 scale bytes of the rows of A (M), of W (N), of A2 (tail_m) and of W2 (N)
   const uint8_t* sa; const uint8_t* sw; const uint8_t* sa2; const uint8_t* sw2;
+  // CONV form (3x3, stride 1, pad 1, NHWC, A = the [B*H*W][C] image with lda = C): image height / width, K-tiles per
+  // tap (C / 64) and its 2^20-scaled reciprocal; per-image row bias rowbias[m / (H*W)][N] (the time embedding)
+  int cv_H, cv_W, cv_lh, cv_lw, cv_ct, cv_recip;  // H, W powers of two (lh / lw their logs), W >= 8
+  const bf16_t* rowbias; long ld_rowbias;
 };
 
 namespace {
@@ -93,10 +97,21 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 // with the waves 4 (M) x 2 (N) as in the 256 x 256 form (32 x 48 = 6 and 32 x 32 = 4 MFMA tiles per wave): per K-tile
 // 10 / 4 / 4 / 4 fragment reads against 12 / 12 / 8 / 8 MFMAs per phase.  The epilogue tile sits in LDS with a 336-B
 // row pitch.  Plain epilogue only, bf16 only.
-template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
+//
+// CONV (256 x 320 only): the 3x3 / stride 1 / pad 1 convolution as an implicit GEMM over the NHWC image (M = B*H*W
+// pixels, K = 9 C ordered [tap][c], C % 64 == 0, H*W % 256 == 0).  A K-tile lies inside one tap (dy, dx), and with
+// stride 1 the source pixel of output row m is m + dy*W + dx: the tap is a wave-uniform shift of the dense form's
+// scalar row base, so the per-lane staging offset stays the one register vA.  A row whose tap falls off its image
+// (oy + dy or ox + dx outside) stages from past the buffer range (zeros).  With W a power of two >= 8 a staged piece
+// (8 rows) never wraps an image row, so oy and the first ox are wave-uniform: a tap off the top / bottom edge drops the
+// whole piece and one off the left / right edge only the piece's first / last row -- two scalar bounds on vA (whose
+// value orders the lane's row inside the piece), no per-lane state.  The A resource starts W + 1 pixels before the
+// image so every source offset is non-negative.
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   static_assert(BN == 256 || ((BN == 160 || BN == 320) && EPI == EPI8_NONE && !FP8),
                 "256 x 160 / 256 x 320 tiles: plain bf16 epilogue only");
+  static_assert(!CONV || BN == 320, "implicit-GEMM conv: 256 x 320 tiles only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
   constexpr int BH0 = BN == 256 ? 128 : (BN == 320 ? 160 : 96), BH1 = BN - BH0;  // rows of the two B images
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // RT (256 x 320): the tail is NOT staged through the ring -- it runs after the main loop from register operands
   // (register budget: the tail's per-lane staging addresses inside the 8-phase loop spill the 160 accumulators)
   constexpr bool RT = BN == 320;
-  const bool has_tail = g.a2 && m0 < g.tail_m;
+  const bool has_tail = g.a2 && m0 < g.tail_m;  // (CONV: a2 is null; a compile-time false here made hipcc spill)
   const int nt2 = (!RT && has_tail) ? (g.K2 + KT - 1) / KT : 0;
   const int nt = (nt1 + nt2 + 1) & ~1;  // the 8-phase loop consumes K-tiles in pairs: an odd count gets a zero tile
 
@@ -161,12 +176,33 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   // base, the half and the K-tile advance are wave-uniform and go in the scalar soffset.  Rows past M read as zeros
   // through rA's range (they are never stored), so no per-lane clamp is needed.
   const unsigned vA = (unsigned)(prow * (int)g.lda * ES + (pch ^ prow) * 16);
+  // CONV: edge bits of the 4 staged pieces (A half h, piece i: pixels p .. p + 7 of one image row, p = m0 + 128 h + 16 w
+  // + 8 i mod H*W) in nibble 2 h + i: top (oy == 0), bottom (oy == H - 1), left (ox == 0), right (ox + 7 == W - 1) --
+  // wave-uniform (W is a power of two >= 8, so a piece never wraps an image row); and the byte step of one image row
+  unsigned cv_edges = 0;
+  int cv_rowb = 0;
+  if constexpr (CONV) {
+    const int hwm = (1 << (g.cv_lh + g.cv_lw)) - 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = (m0 + (r >> 1) * 128 + wave * 16 + (r & 1) * 8) & hwm;
+      const int oy = p >> g.cv_lw, ox0 = p & (g.cv_W - 1);
+      cv_edges |= ((oy == 0 ? 1u : 0u) | (oy == g.cv_H - 1 ? 2u : 0u) | (ox0 == 0 ? 4u : 0u) |
+                   (ox0 == g.cv_W - 8 ? 8u : 0u)) << (4 * r);
+    }
+    cv_rowb = g.cv_W * (int)g.lda * ES;
+  }
   // (256 x 320: the host guarantees lda == ldw, and A's register serves both operands)
+  // (CONV: ldw = 9 lda and 128 | lda * ES, so vW = 9 vA - 8 chunk = vA + 8 (vA & ~127) is formed from vA per staging,
+  // in asm so it is not hoisted into a register of its own: see stage)
   const unsigned vW = BN == 320 ? vA : (unsigned)(prow * (int)g.ldw * ES + (pch ^ prow) * 16);
   // row (inside its image) of this lane in B piece i of this wave (LoRA tail path)
   auto bpiece_row = [&](int i) { return (i < 2 ? wave * 2 + i : 16 + wave) * 8 + prow; };
-  const __amdgpu_buffer_rsrc_t rA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)((long)g.M * g.lda * ES), 0x00020000);
+  // (CONV: the resource starts W + 1 pixels before the image -- offsets of in-image taps are then non-negative -- and
+  // ends W + 1 pixels after it)
+  const long cv_pre = CONV ? (long)(g.cv_W + 1) * g.lda * ES : 0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)g.a - cv_pre), (short)0, (int)((long)g.M * g.lda * ES + 2 * cv_pre), 0x00020000);
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)g.w, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rA2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.a2 ? g.a2 : g.a), (short)0, 0x7fffffff, 0x00020000);
@@ -189,23 +225,59 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
     if (kt < nt1) {
       const int k0 = kt * 128;  // bytes
       if (half < 2) {
-        const int sa = (m0 + (half & 1) * 128 + wave * 16) * (int)g.lda * ES + k0;  // piece 2w, row 0
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, vA, sa, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, vA, sa + 8 * (int)g.lda * ES, 0, 0);
+        if constexpr (CONV) {
+          // K-tile kt = tap * ct + channel block; tap = 3 dy + dx (dy, dx in 0..2 = offsets -1..1)
+          const int tap = (kt * g.cv_recip) >> 20;
+          const int cb = (kt - tap * g.cv_ct) * 128;  // bytes into the pixel's channels
+          const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+          // the tap's edge mask (bit 0: dy = -1 top, 1: dy = +1 bottom, 2: dx = -1 left, 3: dx = +1 right), one nibble
+          // per tap: 5 1 9 / 4 0 8 / 6 2 10
+          const unsigned tm = (unsigned)(0xA26804915ull >> (4 * tap)) & 15u;
+          // piece 2w, row 0 of the shifted source, in the resource's coordinates (which start at pixel -(W + 1))
+          const int sa = (m0 + (half & 1) * 128 + wave * 16) * (int)g.lda * ES + dy * cv_rowb + dx * (int)g.lda * ES + cb;
+          const unsigned rowb = (unsigned)g.lda * ES;  // vA = prow * rowb + chunk: prow == 0 <=> vA < rowb
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            // the piece's edge bits against the tap: top / bottom drop the whole piece, left / right its lane row 0 / 7;
+            // valid <=> lo <= vA <= hm; off = valid ? vA : 0xC0800000 (the inline constant -4.0: past the range, zeros)
+            // -- in asm with the output as the only register (no temporaries: the main loop has none to spare)
+            const unsigned hit = (cv_edges >> (4 * (2 * (half & 1) + i))) & tm;
+            const unsigned lo = (hit & 3u) ? 0x80000000u : ((hit & 4u) ? rowb : 0u);
+            const unsigned hm = (hit & 8u) ? 7u * rowb - 1u : 0x7fffffffu;
+            unsigned off;
+            asm volatile("v_cmp_le_u32 vcc, %1, %3\n\t"
+                         "v_cndmask_b32 %0, -4.0, %3, vcc\n\t"
+                         "v_cmp_ge_u32 vcc, %2, %3\n\t"
+                         "v_cndmask_b32 %0, -4.0, %0, vcc"
+                         : "=&v"(off) : "s"(lo), "s"(hm), "v"(vA) : "vcc");
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + i * 8 * 64), 16, off,
+                                                     sa + i * 8 * (int)g.lda * ES, 0, 0);
+          }
+        } else {
+          const int sa = (m0 + (half & 1) * 128 + wave * 16) * (int)g.lda * ES + k0;  // piece 2w, row 0
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, vA, sa, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, vA, sa + 8 * (int)g.lda * ES, 0,
+                                                   0);
+        }
       } else {
         const int sw = (n0 + (half & 1) * BH0 + wave * 16) * (int)g.ldw * ES + k0;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, vW, sw, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, vW, sw + 8 * (int)g.ldw * ES, 0,
+        unsigned vw = vW;
+        if constexpr (CONV) asm volatile("v_and_b32 %0, 0xffffff80, %1\n\tv_lshl_add_u32 %0, %0, 3, %1" : "=&v"(vw) : "v"(vA));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)dst, 16, vw, sw, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds8_void*)(dst + 8 * 64), 16, vw, sw + 8 * (int)g.ldw * ES, 0,
                                                  0);
         if constexpr (XP)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rW, (lds8_void*)dst_x, 16, vW, ((n0 + (half & 1) * BH0 + (16 + wave) * 8) * (int)g.ldw * ES + k0) | xsrc_oob,
+              rW, (lds8_void*)dst_x, 16, vw, ((n0 + (half & 1) * BH0 + (16 + wave) * 8) * (int)g.ldw * ES + k0) | xsrc_oob,
               0, 0);
       }
     } else if constexpr (RT) {  // the zero pad tile of an odd K-tile count: every load past the buffer range
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, OOB, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, OOB, 0, 0, 0);
-      if (xp) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst_x, 16, OOB, 0, 0, 0);
+      // (the offset materialised in asm at the load: a hoisted constant would hold a register through the main loop)
+      unsigned oob;
+      asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(oob));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst, 16, oob, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)(dst + 8 * 64), 16, oob, 0, 0, 0);
+      if (xp) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds8_void*)dst_x, 16, oob, 0, 0, 0);
     } else {  // LoRA K-tail (one or two K-tiles per output tile) or the zero pad tile
       const int kc = (kt - nt1) * KT + (pch ^ prow) * (16 / ES);  // this lane's 16-B chunk of the tail
       const bool kin = kt < nt1 + nt2 && kc < g.K2;
@@ -493,6 +565,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
           const uint2 v = g.bias ? *reinterpret_cast<const uint2*>(g.bias + n) : make_uint2(0u, 0u);
           bv[jt][0] = bf2f(v.x & 0xffff); bv[jt][1] = bf2f(v.x >> 16);
           bv[jt][2] = bf2f(v.y & 0xffff); bv[jt][3] = bf2f(v.y >> 16);
+          if (CONV && g.rowbias) {  // the tile's image row of the per-image bias (H*W % 256 == 0)
+            const uint2 w = *reinterpret_cast<const uint2*>(g.rowbias + (long)(m0 / (g.cv_H * g.cv_W)) * g.ld_rowbias + n);
+            bv[jt][0] += bf2f(w.x & 0xffff); bv[jt][1] += bf2f(w.x >> 16);
+            bv[jt][2] += bf2f(w.y & 0xffff); bv[jt][3] += bf2f(w.y >> 16);
+          }
         }
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
@@ -737,22 +814,21 @@ static const int g_grid8 = [] {
   return e ? atoi(e) : 256;
 }();
 
-template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256>
+template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256, bool CONV = false>
 int launch8(const Gemm8Args& g, hipStream_t st) {
   const int nblk = ((g.M + 255) / 256) * (g.N / BN);
   // 2 K-tile buffers: 128 KiB (256 x 256) / 104 KiB (256 x 160) / 144 KiB + a 4-KiB dummy slot (256 x 320)
   const size_t shm = (4 * HT + 4 * (BN / 2) * 64 + (BN == 320 ? 4 * 512 : 0)) * sizeof(bf16_t);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN>,
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN, CONV>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     attr_done = true;
   }
-  if (FP8) pso_note_kernel("gemm8p_kernel<%d, true, false, true>", EPI);
-  else if (BN == 160) pso_note_kernel("gemm8p_kernel<0, true, false, false, 160>");
-  else if (BN == 320) pso_note_kernel("gemm8p_kernel<0, true, false, false, 320>");
-  else pso_note_kernel("gemm8p_kernel<%d, %s, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false");
-  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(g);
+  // the demangled name rocprofv3 reports (every template argument), so traces and live attribution agree
+  pso_note_kernel("gemm8p_kernel<%d, %s, %s, %s, %d, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false",
+                  FP8 ? "true" : "false", BN, CONV ? "true" : "false");
+  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN, CONV><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(g);
   return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
 }
 
@@ -820,6 +896,22 @@ int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* 
   g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
   return launch8<EPI8_NONE, true, false, false, 320>(g, st);
+}
+
+// 3x3 / stride 1 / pad 1 implicit-GEMM convolution on 256 x 320 tiles (preconditions checked in gemm.hip: C % 64 == 0,
+// H*W % 256 == 0, Cout % 320 == 0, weight rows [Cout][3][3][C], bf16 output)
+int pso_gemm8p320_conv_run(int B, int H, int W, int C, const void* x, const void* w, int Cout, float alpha,
+                           const void* bias, const void* rowbias, long ld_rowbias, const void* resid, long ldr,
+                           void* out, long ldo, int group_m, hipStream_t st) {
+  Gemm8Args g{};
+  g.a = (const bf16_t*)x; g.lda = C; g.w = (const bf16_t*)w; g.ldw = 9L * C;
+  g.M = B * H * W; g.N = Cout; g.K = 9 * C;
+  g.tail_m = g.M;
+  g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  g.cv_H = H; g.cv_W = W; g.cv_lh = __builtin_ctz(H); g.cv_lw = __builtin_ctz(W); g.cv_ct = C / 64; g.cv_recip = (1 << 20) / (C / 64) + 1;
+  g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias;
+  return launch8<EPI8_NONE, true, false, false, 320, true>(g, st);
 }
 
 // FP8 form (pso_amd.h, pso_gemm_fp8): staggered wave groups, epilogue 0 (bias / alpha / residual) or 1 (GEGLU)

@@ -301,7 +301,7 @@ def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
         sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
         out = sentinel[:M]
         K_.gemm(a, w, bias=b, resid=r, alpha=0.75, out=out, **kw)
-        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 160>"
+        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 160, false>"
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
     finally:
@@ -341,7 +341,7 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
         sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
         out = sentinel[:M]
         K_.gemm(a, w, bias=b, resid=r, alpha=0.75, out=out, **kw)
-        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 320>"
+        assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<0, true, false, false, 320, false>"
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
         # and without bias / residual (the plain store path)
@@ -386,6 +386,39 @@ def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
         assert _rel(din, ref) < 6e-3
     finally:
         K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 44])
+@pytest.mark.parametrize("B,C,H,W,Cout", [(2, 320, 64, 64, 320), (1, 640, 32, 32, 640), (3, 1280, 16, 16, 1280),
+                                          (2, 64, 8, 32, 320), (1, 128, 32, 8, 640), (2, 192, 16, 16, 960)])
+def test_conv_8phase_256x320(cuda, variant, B, C, H, W, Cout):
+    """The 3x3 implicit-GEMM conv on the 8-phase 256 x 320 tiles (gemm8p.hip CONV; variant 44 forces it, the default
+    takes it at >= 256 tiles): bias + per-image row bias + residual, bf16 out, against torch fp32 on the same bf16
+    operands.  The image sits inside a NaN-poisoned buffer (the A resource spans W + 1 pixels either side): a tap
+    that leaked past an image edge, or across images, would read NaN or a neighbour."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(B * C + H * W + Cout)
+    x = torch.randn(B, C, H, W, device=cuda, generator=g).bfloat16()
+    w = (torch.randn(Cout, C, 3, 3, device=cuda, generator=g) / (3 * C ** 0.5)).bfloat16()
+    bias = torch.randn(Cout, device=cuda, generator=g).bfloat16()
+    temb = torch.randn(B, Cout, device=cuda, generator=g).bfloat16()
+    res = torch.randn(B, H, W, Cout, device=cuda, generator=g).bfloat16()
+    ref = (F.conv2d(x.float(), w.float(), bias.float(), padding=1) + temb.float()[:, :, None, None]
+           + _nchw(res.float()))
+    pad = (W + 1 + 64) * C
+    buf = torch.full((B * H * W * C + 2 * pad,), float("nan"), device=cuda).bfloat16()
+    xh = buf[pad:pad + B * H * W * C].view(B, H, W, C)
+    xh.copy_(_nhwc(x))
+    K_.lib().pso_gemm_set_variant(variant)
+    try:
+        out = K_.conv2d(xh, _nhwc(w), bias=bias, rowbias=temb, resid=res)
+        kname = K_.lib().pso_last_kernel().decode()
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+    if variant == 44 or (B * H * W // 256) * (Cout // 320) >= 256:
+        assert kname == "gemm8p_kernel<0, true, false, false, 320, true>", kname
+    assert torch.isfinite(out.float()).all()
+    assert _rel(_nchw(out.float()), ref) < 4e-3
 
 
 @pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
