@@ -777,6 +777,8 @@ int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* 
 int pso_gemm8p320_conv_run(int B, int H, int W, int C, const void* x, const void* w, int Cout, float alpha,
                            const void* bias, const void* rowbias, long ld_rowbias, const void* resid, long ldr,
                            void* out, long ldo, int group_m, hipStream_t st);
+int pso_gemm8p320_geglu_bwd_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* aux,
+                                long ldaux, void* out, long ldo, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 static int g_gemm_variant = 0;
@@ -792,7 +794,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
   const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
-                  gv_raw == 43 || gv_raw == 44)
+                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45)
                      ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
@@ -1293,6 +1295,11 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   g.vec_ok = 1; g.rows_per_group = 1;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   const hipStream_t st = (hipStream_t)stream;
+  // 256 x 320 tiles where they make whole rounds the 256 x 256 ones do not (8192 x 5120: 512 tiles = 2 rounds vs 640 =
+  // 2.5; 32768 x 2560: 1024 = 4 vs 1280 = 5); variant 45 keeps the 256 x 256 form
+  if (g_gemm_variant != 45 && g_gemm_variant != 31 && (N % 320) == 0 && (K % 64) == 0 && lda == ldw && fits30(M, lda) &&
+      fits30(N, ldw) && ((long)((M + 255) / 256) * (N / 320)) % 256 == 0)
+    return pso_gemm8p320_geglu_bwd_run(M, N, K, a, lda, w, ldw, pre, ld_pre, out, ldo, g.group_m, st);
   // 8-phase form (staggered wave groups) by default: 716 vs 658 TF/s for the 2-phase 128x160 kernel at
   // 16384 x 5120 x 1280, 489 vs 472 at 65536 x 2560 x 640 (tools/gemm_bench.py, one box); variant 31 keeps 128x160
   if (g_gemm_variant != 31 && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) &&

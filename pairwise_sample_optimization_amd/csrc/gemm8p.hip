@@ -109,8 +109,9 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 // image so every source offset is non-negative.
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
-  static_assert(BN == 256 || ((BN == 160 || BN == 320) && EPI == EPI8_NONE && !FP8),
-                "256 x 160 / 256 x 320 tiles: plain bf16 epilogue only");
+  static_assert(BN == 256 || ((BN == 160 || BN == 320) && !FP8 && (EPI == EPI8_NONE ||
+                                                                     (BN == 320 && EPI == EPI8_GEGLU_BWD && !CONV))),
+                "256 x 160 / 256 x 320 tiles: bf16, plain epilogue (320: also the GEGLU backward)");
   static_assert(!CONV || BN == 320, "implicit-GEMM conv: 256 x 320 tiles only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
@@ -587,6 +588,42 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       }
     };
     auto store_half = [&](int ha) {
+      if constexpr (EPI == EPI8_GEGLU_BWD) {
+        // the staged half = dout (bf16, as the unfused path stores it); chunk c of row R = dout columns n .. n+7 ->
+        // interleaved input-gradient positions ph .. ph+7 (h) and ph+32 .. (gate), ph = (n / 32) * 64 + n % 32, from
+        // the interleaved pre-activation aux: 128 rows x 40 chunks = 10 passes of 512
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 2
+        for (int p = 0; p < 10; ++p) {
+          const int idx = p * 512 + tid;
+          const int R = idx / 40, c = idx - R * 40, m = m0 + ha * 128 + R;
+          if (m >= g.M) continue;
+          const int n = n0 + c * 8;
+          const int ph = (n >> 5) * 64 + (n & 31);
+          const uint4 dv = *reinterpret_cast<const uint4*>(tl + R * TP + c * 8);
+          const uint4 hv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph);
+          const uint4 gv = *reinterpret_cast<const uint4*>(g.aux + (long)m * g.ldaux + ph + 32);
+          const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, hw[4] = {hv.x, hv.y, hv.z, hv.w},
+                         gw[4] = {gv.x, gv.y, gv.z, gv.w};
+          uint32_t oh[4], og[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d0 = bf2f(dw[e] & 0xffff), d1 = bf2f(dw[e] >> 16);
+            const float h0 = bf2f(hw[e] & 0xffff), h1 = bf2f(hw[e] >> 16);
+            const float q0 = bf2f(gw[e] & 0xffff), q1 = bf2f(gw[e] >> 16);
+            float c0, e0, c1, e1;
+            gelu_erf_parts(q0, c0, e0);
+            gelu_erf_parts(q1, c1, e1);
+            oh[e] = pack2bf(d0 * q0 * c0, d1 * q1 * c1);
+            og[e] = pack2bf(d0 * h0 * (c0 + 0.39894228040143268f * q0 * e0),
+                            d1 * h1 * (c1 + 0.39894228040143268f * q1 * e1));
+          }
+          bf16_t* o = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + ph;
+          *reinterpret_cast<uint4*>(o) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
+          *reinterpret_cast<uint4*>(o + 32) = make_uint4(og[0], og[1], og[2], og[3]);
+        }
+        return;
+      }
       uint4 rvp[10];
 #pragma unroll
       for (int p = 0; p < 10; ++p) {
@@ -896,6 +933,18 @@ int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* 
   g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
   return launch8<EPI8_NONE, true, false, false, 320>(g, st);
+}
+
+// GEGLU backward on 256 x 320 tiles (N % 320 == 0, lda == ldw; preconditions checked in gemm.hip): dout = a . w^T,
+// out = the interleaved [dout * gelu(g) | dout * h * gelu'(g)] from the interleaved pre-activation aux
+int pso_gemm8p320_geglu_bwd_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* aux,
+                                long ldaux, void* out, long ldo, int group_m, hipStream_t st) {
+  Gemm8Args g{};
+  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
+  g.M = M; g.N = N; g.K = K; g.tail_m = M;
+  g.alpha = 1.f; g.out = out; g.ldo = ldo; g.aux = (const bf16_t*)aux; g.ldaux = ldaux;
+  g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  return launch8<EPI8_GEGLU_BWD, true, false, false, 320>(g, st);
 }
 
 // 3x3 / stride 1 / pad 1 implicit-GEMM convolution on 256 x 320 tiles (preconditions checked in gemm.hip: C % 64 == 0,

@@ -352,11 +352,13 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
         K_.lib().pso_gemm_set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 31])
-@pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100)])
+@pytest.mark.parametrize("variant", [0, 31, 45])
+@pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100),
+                                             (8192, 2560, 640, 0)])
 def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
     """The GEGLU projection (interleaved [h | gate] weight rows) and its backward through ff.net.2, on the 8-phase
-    path (default) and the 2-phase one (variant 31), against torch fp32 on the same bf16 operands."""
+    path (default: the backward on 256 x 320 tiles where they make whole rounds), the 8-phase 256 x 256 backward
+    (variant 45) and the 2-phase one (variant 31), against torch fp32 on the same bf16 operands."""
     from pairwise_sample_optimization_amd import kernels as K_
     K_.lib().pso_gemm_set_variant(variant)
     try:
@@ -378,6 +380,8 @@ def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
         wo = (torch.randn(Fd, C, device=cuda, generator=g) / C ** 0.5).bfloat16()
         full_pre = hg[:, idx].bfloat16()
         din = K_.gemm_geglu_bwd(dy, wo, full_pre)
+        if variant == 0 and M in (4096, 8192):  # 256 and 256 tiles of 256 x 320: whole rounds
+            assert K_.lib().pso_last_kernel().decode() == "gemm8p_kernel<2, true, false, false, 320, false>"
         dout = (dy.float() @ wo.float().t()).bfloat16().float()
         hh, gg = h, gt
         cdf = 0.5 * (1 + torch.erf(gg / 2 ** 0.5))
