@@ -141,11 +141,11 @@ def roofline(tr, buf, g):
     from collections import defaultdict
     from pairwise_sample_optimization_amd import kernels as K
     K.PROFILE = []
-    side, K.SideStream.enabled = K.SideStream.enabled, False  # serial launches: each event pair times one kernel alone
+    side, K.SideStream.enabled_any = K.SideStream.enabled_any, False  # serial launches: each event pair times one kernel
     one_step(tr, buf, g)
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
-    K.SideStream.enabled = side
+    K.SideStream.enabled_any = side
     per = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # kernel -> launches, flop, bytes, ms
     for fl, nb, e0, e1, _tag, kname in rec:
         a = per[kname]

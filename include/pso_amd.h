@@ -152,6 +152,14 @@ void pso_attention_set_variant(int v);
  * dB = s dy^T u, reduction over tokens) without materialising transposes; split-K with f32 atomics. */
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream);
+/* pso_gemm_tn with a caller-owned fp32 workspace for the full-weight gradients (C3 / C4: both sides >= 128 wide):
+ * when the 128 x 128 tiles alone leave CUs idle (I x J <= ~2 M, e.g. the 640^2 / 1280^2 weights), the reduction
+ * rows are split over up to ws_bytes / (4 I J) slices whose partial products are STORED into ws and added into out
+ * in slice order by a second kernel (deterministic; no f32 atomics).  pso_gemm_tn_ws_bytes(M, I, J) = the bytes
+ * that enable the full split (0: no split applies); a smaller workspace gives fewer slices, 0 = pso_gemm_tn. */
+size_t pso_gemm_tn_ws_bytes(int M, int I, int J);
+int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                   long ldo, void* ws, size_t ws_bytes, void* stream);
 /* Grouped (block-diagonal) form of pso_gemm_tn for the fused q/k/v LoRA adapters: with A = [M][I] the big side and
  * B = [M][J] the rank side (J = r * I / group), out[i][j] += alpha * sum_m A[m][i] B[m][(i / group) * r + j % r]
  * restricted to j in that group's r columns (out is [I][r]).  group = 0: plain pso_gemm_tn. */

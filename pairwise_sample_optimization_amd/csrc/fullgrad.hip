@@ -74,6 +74,98 @@ __global__ __launch_bounds__(256) void ln_dparam_kernel(int M, int C, const bf16
   }
 }
 
+// Vector forms (N % 8 == 0, 16-B aligned rows): 256 threads = 4 row slices x 64 chunks of 8 columns (16-B loads), a
+// block = CS2_ROWS rows x 512 columns, so even the smallest weight (6144 x 1280 rows x columns of one image group) has
+// ~300 blocks in flight; the 4 slices are summed in LDS and one atomic per column leaves the block (a block that
+// straddles a row group -- per-image sums -- flushes per thread instead).
+constexpr int CS2_ROWS = 64;
+
+__device__ __forceinline__ void unpack8f(const uint4 v, float (&f)[8]) {
+  f[0] = bf2f(v.x & 0xffff); f[1] = bf2f(v.x >> 16); f[2] = bf2f(v.y & 0xffff); f[3] = bf2f(v.y >> 16);
+  f[4] = bf2f(v.z & 0xffff); f[5] = bf2f(v.z >> 16); f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
+}
+
+// NS sums per column (colsum: 1, LN dparam: 2) of the block's slices -> LDS -> one atomic each per column, the
+// block's 512 columns 2 per thread in column order (each wave-instruction adds 64 consecutive floats: 4 atomic
+// requests of 64 B; a lane-per-8-columns order would scatter every lane into its own 64-B request)
+template <int NS>
+__device__ __forceinline__ void cs2_flush(float (&acc)[NS][8], float* __restrict__ o0, float* __restrict__ o1, int nb,
+                                          int N, float (*red)[4][64][8]) {
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[k][ty][tx][e] = acc[k][e];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = h * 256 + t, n = nb + c;  // column c of the block
+    if (n >= N) continue;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const float v = red[k][0][c >> 3][c & 7] + red[k][1][c >> 3][c & 7] + red[k][2][c >> 3][c & 7] +
+                      red[k][3][c >> 3][c & 7];
+      atomicAdd((k ? o1 : o0) + n, v);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum8_kernel(long M, int N, const bf16_t* __restrict__ x, long ldx, long rpg,
+                                                      float* __restrict__ out, long ldo) {
+  __shared__ float red[1][4][64][8];
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+  const int n = (blockIdx.x * 64 + tx) * 8;
+  const long r0 = (long)blockIdx.y * CS2_ROWS, r1 = min(M, r0 + CS2_ROWS);
+  const bool straddle = r0 / rpg != (r1 - 1) / rpg;  // block-uniform
+  float acc[1][8] = {{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+  long cur = r0 / rpg;
+  if (n < N) {
+    for (long m = r0 + ty; m < r1; m += 4) {
+      if (straddle && m / rpg != cur) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { atomicAdd(out + cur * ldo + n + e, acc[0][e]); acc[0][e] = 0.f; }
+        cur = m / rpg;
+      }
+      float f[8];
+      unpack8f(*reinterpret_cast<const uint4*>(x + m * ldx + n), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[0][e] += f[e];
+    }
+  }
+  if (straddle) {
+    if (n < N)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(out + cur * ldo + n + e, acc[0][e]);
+    return;
+  }
+  cs2_flush<1>(acc, out + cur * ldo, nullptr, blockIdx.x * 512, N, red);
+}
+
+__global__ __launch_bounds__(256) void ln_dparam8_kernel(int M, int C, const bf16_t* __restrict__ x, long ldx,
+                                                         const bf16_t* __restrict__ dy, long lddy,
+                                                         const float* __restrict__ stats, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta) {
+  __shared__ float red[2][4][64][8];
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+  const int c = (blockIdx.x * 64 + tx) * 8;
+  const int r0 = blockIdx.y * CS2_ROWS, r1 = min(M, r0 + CS2_ROWS);
+  float acc[2][8] = {{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+  if (c < C) {
+    for (int m = r0 + ty; m < r1; m += 4) {
+      const float2 st = *reinterpret_cast<const float2*>(stats + 2 * m);
+      float xs[8], ds[8];
+      unpack8f(*reinterpret_cast<const uint4*>(x + (long)m * ldx + c), xs);
+      unpack8f(*reinterpret_cast<const uint4*>(dy + (long)m * lddy + c), ds);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[0][e] += ds[e] * (xs[e] - st.x) * st.y;
+        acc[1][e] += ds[e];
+      }
+    }
+  }
+  cs2_flush<2>(acc, dgamma, dbeta, blockIdx.x * 512, C, red);
+}
+
 // one thread per (output pixel, tap, 8-channel chunk)
 __global__ __launch_bounds__(256) void im2col_conv_kernel(int mode, int B, const bf16_t* __restrict__ s1, int C1,
                                                           const bf16_t* __restrict__ s2, int C2, int H, int W, int Ho,
@@ -121,6 +213,11 @@ int pso_colsum_acc(long M, int N, const void* x, long ldx, long rows_per_group, 
   PSO_ARG_CHECK(M >= 0 && N > 0 && x && out && rows_per_group > 0, "pso_colsum_acc: bad arguments");
   PSO_ARG_CHECK((((uintptr_t)x) & 7) == 0 && (ldx % 4) == 0, "pso_colsum_acc: 8-B aligned rows");
   if (M == 0) return PSO_OK;
+  if ((N % 8) == 0 && (((uintptr_t)x) & 15) == 0 && (ldx % 8) == 0) {
+    const dim3 grid((N + 511) / 512, (unsigned)((M + CS2_ROWS - 1) / CS2_ROWS));
+    colsum8_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, N, (const bf16_t*)x, ldx, rows_per_group, out, ldo);
+    return pso_check_launch("pso_colsum_acc");
+  }
   const dim3 grid((N + 255) / 256, (unsigned)((M + CS_ROWS - 1) / CS_ROWS));
   colsum_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, N, (const bf16_t*)x, ldx, rows_per_group, out, ldo);
   return pso_check_launch("pso_colsum_acc");
@@ -133,6 +230,13 @@ int pso_layer_norm_dparam(int M, int C, const void* x, long ldx, const void* dy,
   PSO_ARG_CHECK((((uintptr_t)x) & 7) == 0 && (((uintptr_t)dy) & 7) == 0 && (ldx % 4) == 0 && (lddy % 4) == 0,
                 "pso_layer_norm_dparam: 8-B aligned rows");
   if (M == 0) return PSO_OK;
+  if ((C % 8) == 0 && ((((uintptr_t)x) | ((uintptr_t)dy)) & 15) == 0 && (ldx % 8) == 0 && (lddy % 8) == 0 &&
+      (((uintptr_t)stats) & 7) == 0) {
+    const dim3 grid((C + 511) / 512, (M + CS2_ROWS - 1) / CS2_ROWS);
+    ln_dparam8_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy,
+                                                            stats, dgamma, dbeta);
+    return pso_check_launch("pso_layer_norm_dparam");
+  }
   const dim3 grid((C + 255) / 256, (M + CS_ROWS - 1) / CS_ROWS);
   ln_dparam_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
                                                          dgamma, dbeta);

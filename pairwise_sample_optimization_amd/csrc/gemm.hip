@@ -1066,7 +1066,7 @@ __device__ __forceinline__ s16x4 tn_tr_asm(unsigned img_base, int r0, int col0, 
 __global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J, const bf16_t* __restrict__ A,
                                                             long lda, const bf16_t* __restrict__ B, long ldb,
                                                             float alpha, float* __restrict__ out, long ldo,
-                                                            int steps) {
+                                                            int steps, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) bf16_t sT[2][4][64 * 64];  // [stage][A0 A1 B0 B1], 64 KB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1153,7 +1153,10 @@ __global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J,
       const int j = j0 + wj * 64 + b * 16 + 4 * g;
       if (j >= J) continue;  // J % 8 == 0: a lane's 4 columns are all in or all out
       float* o = out + (long)i * ldo + j;
-      if (gridDim.y > 1) {
+      if (part) {  // this slice's partial product, stored (added into out by tn_reduce_slices_kernel)
+        *reinterpret_cast<float4*>(part + ((long)blockIdx.y * I + i) * J + j) =
+            make_float4(acc[a][b][0] * alpha, acc[a][b][1] * alpha, acc[a][b][2] * alpha, acc[a][b][3] * alpha);
+      } else if (gridDim.y > 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) atomicAdd(o + r, acc[a][b][r] * alpha);
       } else {
@@ -1164,7 +1167,71 @@ __global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J,
   }
 }
 
+// out[i][j] += sum over the ks slices of part[s][i][j], in slice order (4 consecutive j per thread)
+__global__ void tn_reduce_slices_kernel(int I, int J, int ks, const float* __restrict__ part, float* __restrict__ out,
+                                        long ldo) {
+  const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long n4 = (long)I * J / 4;
+  if (q >= n4) return;
+  const long e = q * 4;
+  const int i = (int)(e / J), j = (int)(e - (long)i * J);
+  float4 sacc = *reinterpret_cast<const float4*>(part + e);
+  for (int sl = 1; sl < ks; ++sl) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long)sl * I * J + e);
+    sacc.x += v.x; sacc.y += v.y; sacc.z += v.z; sacc.w += v.w;
+  }
+  float* o = out + (long)i * ldo + j;
+  o[0] += sacc.x; o[1] += sacc.y; o[2] += sacc.z; o[3] += sacc.w;
+}
+
+// split of the full-weight TN product into ks slices of the reduction rows for the workspace form: enough slices for
+// ~1.5 rounds of 128 x 128 tiles over the 256 CUs, each slice >= 8 K-steps (512 rows)
+static int tn_ws_slices(int M, int I, int J) {
+  if (I < 128 || J < 128) return 0;
+  const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
+  if (t128 >= 256) return 0;
+  const int nkt = (M + 63) / 64;
+  int ks = (384 + t128 - 1) / t128;
+  if (ks > nkt / 8) ks = nkt / 8;
+  return ks >= 2 ? ks : 0;
+}
+
 extern "C" {
+
+size_t pso_gemm_tn_ws_bytes(int M, int I, int J) {
+  const int ks = tn_ws_slices(M, I, J);
+  return ks ? (size_t)ks * I * J * sizeof(float) : 0;
+}
+
+int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                   long ldo, void* ws, size_t ws_bytes, void* stream) {
+  int ks = tn_ws_slices(M, I, J);
+  if (ks && ws && (ldo % 4) == 0 && (((uintptr_t)out) & 15) == 0 && (((uintptr_t)ws) & 15) == 0 && (J % 4) == 0 &&
+      (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30) && g_tn_split == 0) {
+    PSO_ARG_CHECK(M >= 0 && A && B && out, "pso_gemm_tn_ws: bad args");
+    PSO_ARG_CHECK(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && (lda % 8) == 0 && (ldb % 8) == 0 &&
+                      (I % 8) == 0 && (J % 8) == 0,
+                  "pso_gemm_tn_ws: operands need 16-B aligned rows and I, J multiples of 8");
+    const long slice = (long)I * J * (long)sizeof(float);
+    if ((long)ws_bytes / slice < ks) ks = (int)((long)ws_bytes / slice);
+    if (ks >= 2) {
+      const int nkt = (M + 63) / 64;
+      const int steps = (nkt + ks - 1) / ks;
+      ks = (nkt + steps - 1) / steps;
+      const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
+      pso_note_kernel("gemm_tn128_kernel");
+      gemm_tn128_kernel<<<dim3(t128, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda,
+                                                                          (const bf16_t*)B, ldb, alpha, out, ldo,
+                                                                          steps, (float*)ws);
+      const long n4 = (long)I * J / 4;
+      tn_reduce_slices_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(I, J, ks,
+                                                                                            (const float*)ws, out,
+                                                                                            ldo);
+      return pso_check_launch("pso_gemm_tn_ws");
+    }
+  }
+  return pso_gemm_tn_grouped(M, I, J, A, lda, B, ldb, alpha, out, ldo, 0, stream);
+}
 
 int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
@@ -1370,7 +1437,8 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   if (t128 * ks >= 128) {
     pso_note_kernel("gemm_tn128_kernel");
     gemm_tn128_kernel<<<dim3(t128, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda,
-                                                                        (const bf16_t*)B, ldb, alpha, out, ldo, steps);
+                                                                        (const bf16_t*)B, ldb, alpha, out, ldo, steps,
+                                                                        nullptr);
     return pso_check_launch("pso_gemm_tn");
   }
   }

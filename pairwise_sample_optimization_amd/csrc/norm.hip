@@ -178,6 +178,44 @@ __global__ void gn_dparam_kernel(int B, int C, int nchunks, const float* __restr
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
 }
 
+// The same sums spread over the chip: block (64 channels, split s of S) adds the (image, chunk) entries s, s + S, ...
+// in 4 slices (fp64, summed in LDS) into part2[s][c][2] (doubles); gn_dparam_final_kernel adds the S partials per
+// channel in fixed order.  (The one-pass form above runs C / 128 workgroups -- 3 for 320 channels -- each walking every
+// entry: ~130 us per call in the full-UNet backward.)
+__global__ __launch_bounds__(256) void gn_dparam_split_kernel(int BK, int C, int S, const float* __restrict__ ws,
+                                                              double* __restrict__ part2) {
+  __shared__ double red[4][64][2];
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+  const int c = blockIdx.x * 64 + tx, sp = blockIdx.y;
+  double a = 0.0, q = 0.0;
+  if (c < C)
+    for (int e = sp + S * ty; e < BK; e += 4 * S) {
+      const float2 v = *reinterpret_cast<const float2*>(ws + ((size_t)e * C + c) * 2);
+      a += v.x;
+      q += v.y;
+    }
+  red[ty][tx][0] = a;
+  red[ty][tx][1] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    part2[((size_t)sp * C + c) * 2] = red[0][tx][0] + red[1][tx][0] + red[2][tx][0] + red[3][tx][0];
+    part2[((size_t)sp * C + c) * 2 + 1] = red[0][tx][1] + red[1][tx][1] + red[2][tx][1] + red[3][tx][1];
+  }
+}
+
+__global__ void gn_dparam_final_kernel(int C, int S, const double* __restrict__ part2, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, q = 0.0;
+  for (int sp = 0; sp < S; ++sp) {
+    a += part2[((size_t)sp * C + c) * 2];
+    q += part2[((size_t)sp * C + c) * 2 + 1];
+  }
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)a;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
+}
+
 // Apply passes: block = (pixel chunk of GN_ROWS, image) like the partial pass; thread (row slot, 8-channel chunk) folds
 // mean / rstd / gamma / beta of its 8 channels into per-channel (scale, shift) once and streams its pixel rows with
 // one FMA (+ SiLU) per element -- no per-element divisions or scalar parameter loads.
@@ -428,8 +466,18 @@ int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* d
     gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part,
                                                                            part_ch);
   gn_finalize_kernel<true><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, coef);
-  if (dgamma || dbeta)
-    gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part_ch, dgamma, dbeta, accumulate_dparams);
+  if (dgamma || dbeta) {
+    // the group partials (part) are consumed by gn_finalize above: their space takes the split sums (S <= B*chunks/2
+    // doubles per channel pair fit in B*chunks*C*2 floats)
+    const int BK = B * nchunks, S = BK >= 64 ? 32 : BK / 2;
+    if (S >= 2) {
+      gn_dparam_split_kernel<<<dim3(cdiv(C, 64), S), 256, 0, st>>>(BK, C, S, part_ch, (double*)part);
+      gn_dparam_final_kernel<<<cdiv(C, 128), 128, 0, st>>>(C, S, (const double*)part, dgamma, dbeta,
+                                                           accumulate_dparams);
+    } else {
+      gn_dparam_kernel<<<cdiv(C, 128), 128, 0, st>>>(B, C, nchunks, part_ch, dgamma, dbeta, accumulate_dparams);
+    }
+  }
   if (silu)
     gn_apply_bwd_kernel<true><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, xp, dyp, stats, coef, gp, bp,
                                                                     (const bf16_t*)dadd, (bf16_t*)dx);

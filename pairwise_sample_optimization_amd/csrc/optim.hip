@@ -80,7 +80,7 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
 // m and v live as uint8 codes into two 256-entry dynamic quantisation maps (signed for m, unsigned for v) with one
 // fp32 absmax per 2048-element block; each step dequantises with the previous absmax, updates, and requantises
 // (nearest code) against the block's new absmax.  One 256-thread workgroup per block, 8 consecutive elements per
-// thread; the maps travel in the kernel arguments and sit in LDS.  Arithmetic in the order of bitsandbytes'
+// thread (32-B / 8-B vector loads and stores); the maps travel in the kernel arguments and sit in LDS.  Arithmetic in the order of bitsandbytes'
 // kOptimizerStatic8bit2StateBlockwise ADAM branch (restated in oracle/adam8bit.py, parity unpinned: no bitsandbytes
 // here), contraction off so the fp32 rounding matches the restatement step for step.
 #define ADAM8_BLOCK 2048
@@ -88,17 +88,25 @@ struct Adam8Maps {
   float s[256], u[256];
 };
 
-__device__ __forceinline__ int adam8_nearest(const float* __restrict__ code, float x) {
-  // lower_bound over the sorted map, then the nearer of the two neighbours (ties -> the lower index)
-  int lo = 0, n = 256;
-  while (n > 0) {
-    const int h = n >> 1;
-    if (code[lo + h] < x) { lo += h + 1; n -= h + 1; }
-    else n = h;
+// nearest code of x in a sorted 256-entry map (ties -> the lower index): the count of entries below x by a branch-free
+// 8-step search (equal to lower_bound except that it stops at 255, which the clamp below maps to the same index), then
+// the nearer neighbour.  The searches of a thread's 16 values run in lockstep (adam8_nearest16), so every step issues
+// 16 independent LDS reads instead of one dependent chain per value.
+template <int NV>
+__device__ __forceinline__ void adam8_nearest16(const float* __restrict__ code, const float (&x)[NV], int (&idx)[NV]) {
+  int lo[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) lo[k] = 0;
+#pragma unroll
+  for (int h = 128; h > 0; h >>= 1)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lo[k] += code[lo[k] + h - 1] < x[k] ? h : 0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lo[k] < 1 ? 1 : lo[k];
+    const float a = code[i - 1], b = code[i];
+    idx[k] = fabsf(x[k] - a) <= fabsf(b - x[k]) ? i - 1 : i;
   }
-  int idx = lo < 1 ? 1 : (lo > 255 ? 255 : lo);
-  const float a = code[idx - 1], b = code[idx];
-  return fabsf(x - a) <= fabsf(b - x) ? idx - 1 : idx;
 }
 
 __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
@@ -115,21 +123,43 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   cu[t] = maps.u[t];
   const long blk = blockIdx.x;
   const long i0 = blk * ADAM8_BLOCK + (long)t * 8;
+  const bool full = i0 + 8 <= n;  // every thread of a block but the last block's tail: 32-B / 8-B vector accesses
   const float s = gscale * (clip ? clip[1] : 1.0f);
   const float am0 = am[blk], av0 = av[blk];
+  float gv[8], pv[8];
+  uint32_t cm[2], cv[2];
+  if (full) {
+    const float4 g0 = *reinterpret_cast<const float4*>(g + i0), g1 = *reinterpret_cast<const float4*>(g + i0 + 4);
+    const float4 p0 = *reinterpret_cast<const float4*>(p + i0), p1 = *reinterpret_cast<const float4*>(p + i0 + 4);
+    const uint2 qa = *reinterpret_cast<const uint2*>(qm + i0), qb = *reinterpret_cast<const uint2*>(qv + i0);
+    gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
+    pv[0] = p0.x; pv[1] = p0.y; pv[2] = p0.z; pv[3] = p0.w; pv[4] = p1.x; pv[5] = p1.y; pv[6] = p1.z; pv[7] = p1.w;
+    cm[0] = qa.x; cm[1] = qa.y; cv[0] = qb.x; cv[1] = qb.y;
+  } else {
+    cm[0] = cm[1] = cv[0] = cv[1] = 0u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long i = i0 + e;
+      gv[e] = i < n ? g[i] : 0.f;
+      pv[e] = i < n ? p[i] : 0.f;
+      if (i < n) {
+        cm[e >> 2] |= (uint32_t)qm[i] << (8 * (e & 3));
+        cv[e >> 2] |= (uint32_t)qv[i] << (8 * (e & 3));
+      }
+    }
+  }
   __syncthreads();
-  float m[8], v[8], pv[8];
+  float m[8], v[8];
   float mx_m = 0.f, mx_v = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const long i = i0 + e;
-    if (i < n) {
-      const float gi = g[i] * s;
-      m[e] = cs[qm[i]] * am0;
-      v[e] = cu[qv[i]] * av0;
+    if (full || i0 + e < n) {
+      const float gi = gv[e] * s;
+      m[e] = cs[(cm[e >> 2] >> (8 * (e & 3))) & 255u] * am0;
+      v[e] = cu[(cv[e >> 2] >> (8 * (e & 3))) & 255u] * av0;
       m[e] = (m[e] * b1) + (omb1 * gi);
       v[e] = (v[e] * b2) + ((omb2 * gi) * gi);
-      pv[e] = p[i] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
+      pv[e] = pv[e] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
       pv[e] = pv[e] * decay;
       mx_m = fmaxf(mx_m, fabsf(m[e]));
       mx_v = fmaxf(mx_v, fabsf(v[e]));
@@ -147,13 +177,33 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   __syncthreads();
   const float nm = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
   const float nv = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  float xm[8], xv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const long i = i0 + e;
-    if (i >= n) continue;
-    p[i] = pv[e];
-    qm[i] = (uint8_t)adam8_nearest(cs, nm > 0.f ? m[e] / nm : 0.f);
-    qv[i] = (uint8_t)adam8_nearest(cu, nv > 0.f ? v[e] / nv : 0.f);
+    xm[e] = nm > 0.f ? m[e] / nm : 0.f;
+    xv[e] = nv > 0.f ? v[e] / nv : 0.f;
+  }
+  int im[8], iv[8];
+  adam8_nearest16(cs, xm, im);
+  adam8_nearest16(cu, xv, iv);
+  if (full) {
+    *reinterpret_cast<float4*>(p + i0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    *reinterpret_cast<float4*>(p + i0 + 4) = make_float4(pv[4], pv[5], pv[6], pv[7]);
+    *reinterpret_cast<uint2*>(qm + i0) =
+        make_uint2((uint32_t)im[0] | (uint32_t)im[1] << 8 | (uint32_t)im[2] << 16 | (uint32_t)im[3] << 24,
+                   (uint32_t)im[4] | (uint32_t)im[5] << 8 | (uint32_t)im[6] << 16 | (uint32_t)im[7] << 24);
+    *reinterpret_cast<uint2*>(qv + i0) =
+        make_uint2((uint32_t)iv[0] | (uint32_t)iv[1] << 8 | (uint32_t)iv[2] << 16 | (uint32_t)iv[3] << 24,
+                   (uint32_t)iv[4] | (uint32_t)iv[5] << 8 | (uint32_t)iv[6] << 16 | (uint32_t)iv[7] << 24);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long i = i0 + e;
+      if (i >= n) continue;
+      p[i] = pv[e];
+      qm[i] = (uint8_t)im[e];
+      qv[i] = (uint8_t)iv[e];
+    }
   }
   if (t == 0) { am[blk] = nm; av[blk] = nv; }
 }
@@ -257,6 +307,8 @@ int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg
                        float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
   PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0,
                 "pso_adamw8bit_step: bad args");
+  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
+                "pso_adamw8bit_step: param / grad need 16-B, the code arrays 8-B alignment");
   static Adam8Maps maps = [] {
     Adam8Maps m;
     adam8_dynamic_map(true, m.s);

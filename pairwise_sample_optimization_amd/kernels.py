@@ -46,12 +46,15 @@ class SideStream:
 
     enabled = os.environ.get("PSO_SIDE_STREAM", "0") == "1"  # measured neutral on the C2 step (31.35 vs 31.44 imgs/s)
 
-    def __init__(self):
+    def __init__(self, enabled=None):
+        """enabled: None = the class default (PSO_SIDE_STREAM); the full-UNet backward turns it on for its weight
+        gradients (PSO_FULL_SIDE_STREAM=0 keeps them in line)."""
+        self.on = SideStream.enabled if enabled is None else enabled
         self.s = None
         self.pending = False
 
     def launch(self, fn, *tensors):
-        if not self.enabled:
+        if not (self.on and SideStream.enabled_any):
             fn()
             return
         main = torch.cuda.current_stream()
@@ -68,6 +71,9 @@ class SideStream:
         if self.pending:
             torch.cuda.current_stream().wait_stream(self.s)
             self.pending = False
+
+
+SideStream.enabled_any = True  # False: every launch in line (profiling with serial event timing, bench.roofline)
 
 
 def _row_stride(t):
@@ -139,11 +145,18 @@ def gemm_grouped_skinny(a, w, groups, out=None, alpha=1.0):
     return out
 
 
+_GEGLU_IDX = {}
+
+
 def geglu_interleave_index(F, device=None):
-    """Row order of the GEGLU proj weight for the fused epilogue: per 32 outputs, [h rows 32 | gate rows 32]."""
-    g = torch.arange(F // 32, device=device).view(-1, 1)
-    j = torch.arange(32, device=device).view(1, -1)
-    return torch.cat([g * 32 + j, F + g * 32 + j], 1).reshape(-1)
+    """Row order of the GEGLU proj weight for the fused epilogue: per 32 outputs, [h rows 32 | gate rows 32].
+    Cached per (F, device): the full-UNet backward and every re-prepare ask for it again."""
+    key = (F, str(device))
+    if key not in _GEGLU_IDX:
+        g = torch.arange(F // 32, device=device).view(-1, 1)
+        j = torch.arange(32, device=device).view(1, -1)
+        _GEGLU_IDX[key] = torch.cat([g * 32 + j, F + g * 32 + j], 1).reshape(-1)
+    return _GEGLU_IDX[key]
 
 
 def gemm_geglu(a, w_int, b_int, out_pre=None, out=None, pre_rows=0):
@@ -232,7 +245,7 @@ def gemm_fp8(a, w, *, a2=None, w2=None, tail_rows=0, tail_group_n=0, alpha=1.0, 
 TN_RANKS = (32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
 
 
-def gemm_tn(a, b, out, alpha=1.0, group=0):
+def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
     """out[I,J] (f32, accumulated) += alpha * a^T @ b  with a [M,I], b [M,J] (row-strided views).
     group > 0 (block-diagonal, fused q/k/v adapters): out [I, r] with r = J * group / I; column block
     a[:, g*group:(g+1)*group] pairs with b[:, g*r:(g+1)*r]."""
@@ -241,8 +254,14 @@ def gemm_tn(a, b, out, alpha=1.0, group=0):
     r = J * group // I if group else J
     assert b.shape[0] == M and out.shape == (I, r) and out.dtype == torch.float32
     e0 = _prof_begin()
-    check(lib().pso_gemm_tn_grouped(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
-                                    _row_stride(out), int(group), stream_ptr()), "pso_gemm_tn")
+    wsb = lib().pso_gemm_tn_ws_bytes(M, I, J) if group == 0 and split_ws else 0
+    if wsb:  # full-weight gradient with few 128 x 128 tiles: split rows, ordered reduction through a workspace
+        ws = torch.empty(wsb, device=a.device, dtype=torch.uint8)
+        check(lib().pso_gemm_tn_ws(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha), ptr(out),
+                                   _row_stride(out), ptr(ws), wsb, stream_ptr()), "pso_gemm_tn_ws")
+    else:
+        check(lib().pso_gemm_tn_grouped(M, I, J, ptr(a), _row_stride(a), ptr(b), _row_stride(b), float(alpha),
+                                        ptr(out), _row_stride(out), int(group), stream_ptr()), "pso_gemm_tn")
     _prof_end(e0, 2.0 * M * I * r, 2.0 * M * (I + J) + 8.0 * I * r, ("gemm_tn", M, I, J, group))
     return out
 

@@ -173,54 +173,95 @@ class FullGradState:
         order += [nm for nm in named if nm not in seen]
         self.names = order
         params = [named[nm] for nm in order]
-        n = sum(p.numel() for p in params)
+        # every tensor starts on a 64-element boundary of the flat buffers (its bf16 working view then has the 16-B
+        # aligned rows the kernels need); the pads are zero in master and grad and stay zero under the optimizer
+        slot = lambda k: -(-k // self.ALIGN) * self.ALIGN
+        n = sum(slot(p.numel()) for p in params)
         dev = params[0].device
         self.params = params
-        self.master = torch.empty(n, device=dev, dtype=torch.float32)
+        self.master = torch.zeros(n, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(n, device=dev, dtype=torch.float32)
+        # the bf16 module weights become views of ONE flat working copy in the master's layout, so refresh() is one
+        # cast kernel (it was one copy per tensor: ~1,700 launches per optimizer step)
+        assert all(p.dtype == params[0].dtype for p in params), "full-UNet training needs one parameter dtype"
+        self.work = torch.zeros(n, device=dev, dtype=params[0].dtype)
         self._g, self._m = {}, {}
-        off = 0
-        for p in params:
-            k = p.numel()
-            self._m[id(p)] = self.master[off:off + k].view(p.shape)
-            self._g[id(p)] = self.grad[off:off + k].view(p.shape)
-            self._m[id(p)].copy_(p.data.float())
-            off += k
-        self.numel = n
         self.offsets = {}
         off = 0
         for nm, p in zip(order, params):
-            self.offsets[nm] = (off, p.numel())
-            off += p.numel()
+            k = p.numel()
+            self.offsets[nm] = (off, slot(k))  # the slot (with its pad): units of them tile the flat buffers
+            self._m[id(p)] = self.master[off:off + k].view(p.shape)
+            self._g[id(p)] = self.grad[off:off + k].view(p.shape)
+            self._m[id(p)].copy_(p.data.float())
+            w = self.work[off:off + k].view(p.shape)
+            w.copy_(p.data)
+            p.data = w
+            off += slot(k)
+        self.numel = n
         self.trigger = torch.zeros(1, device=dev, requires_grad=True)  # autograd hook for UNet.forward (_UNetFn)
+
+    ALIGN = 64  # elements per flat-buffer slot boundary
 
     def g(self, p):
         """fp32 gradient view of module parameter p (same shape)."""
         return self._g[id(p)]
 
-    def refresh(self):
-        """master -> bf16 module weights (the caller re-runs prepare())."""
+    def master_from_params(self):
+        """bf16 module weights -> fp32 master (after the weights were changed in place)."""
         with torch.no_grad():
-            for p in self.params:
-                p.data.copy_(self._m[id(p)])
+            K.cast_bf16_f32(self.work, out=self.master)
+
+    def refresh(self):
+        """master -> bf16 module weights (the caller re-runs prepare()): one cast over the flat buffers."""
+        with torch.no_grad():
+            K.cast_f32_bf16(self.master, out=self.work)
 
 
-def _lin_dw(fg, lin, dy, x):
-    """nn.Linear weight / bias grads: dW += dy^T x (TN GEMM), db += column sums of dy."""
-    K.gemm_tn(dy, x, fg.g(lin.weight))
-    if lin.bias is not None:
-        K.colsum_acc(dy, fg.g(lin.bias).view(1, -1))
+_FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
 
 
-def _conv_dw(fg, conv, dy2d, cols):
-    """3x3 conv weight / bias grads from the patch matrix cols [M, 9*Cin] (tap-major): dW_nhwc = dy^T cols, then
-    into the diffusers [Cout][Cin][kh][kw] grad view."""
-    tmp = torch.zeros((dy2d.shape[1], cols.shape[1]), device=cols.device, dtype=torch.float32)
-    K.gemm_tn(dy2d, cols, tmp)
-    co = conv.cout
-    fg.g(conv.weight).add_(tmp[:co, :9 * conv.cin].view(co, 3, 3, conv.cin).permute(0, 3, 1, 2))
-    if conv.bias is not None:
-        K.colsum_acc(dy2d[:, :co] if dy2d.shape[1] != co else dy2d, fg.g(conv.bias).view(1, -1))
+def _lin_dw(fg, lin, dy, x, rt=None):
+    """nn.Linear weight / bias grads: dW += dy^T x (TN GEMM), db += column sums of dy (on rt's side stream)."""
+    def run():
+        K.gemm_tn(dy, x, fg.g(lin.weight))
+        if lin.bias is not None:
+            K.colsum_acc(dy, fg.g(lin.bias).view(1, -1))
+    if rt is None:
+        run()
+    else:
+        rt.side.launch(run, dy, x)
+
+
+def _conv_dw(fg, conv, dy2d, src, rt=None, cols_fn=None):
+    """3x3 conv weight / bias grads from the patch matrix cols [M, 9*Cin] (tap-major) = cols_fn(src): dW_nhwc =
+    dy^T cols, then into the diffusers [Cout][Cin][kh][kw] grad view (the patch matrix is built on rt's side stream
+    too).  cols_fn None: src is the patch matrix."""
+    def run():
+        cols = cols_fn(src) if cols_fn is not None else src
+        tmp = torch.zeros((dy2d.shape[1], cols.shape[1]), device=cols.device, dtype=torch.float32)
+        K.gemm_tn(dy2d, cols, tmp)
+        co = conv.cout
+        fg.g(conv.weight).add_(tmp[:co, :9 * conv.cin].view(co, 3, 3, conv.cin).permute(0, 3, 1, 2))
+        if conv.bias is not None:
+            K.colsum_acc(dy2d[:, :co] if dy2d.shape[1] != co else dy2d, fg.g(conv.bias).view(1, -1))
+    if rt is None:
+        run()
+    else:
+        rt.side.launch(run, dy2d, src)
+
+
+def _tn_stacked(fg, lins, dy, x):
+    """dW of nn.Linears whose weights are stacked rows of one flat-gradient range (q / k / v; cross k / v) fed by the
+    column blocks of one dy: ONE TN GEMM over the stacked rows when their grads are adjacent, else one per weight."""
+    gs = [fg.g(l.weight) for l in lins]
+    n = gs[0].numel()
+    if all(g.data_ptr() == gs[0].data_ptr() + i * n * 4 for i, g in enumerate(gs)):
+        K.gemm_tn(dy, x, gs[0].view(-1).as_strided((len(gs) * gs[0].shape[0], gs[0].shape[1]), (gs[0].shape[1], 1)))
+    else:
+        C = gs[0].shape[0]
+        for j, g in enumerate(gs):
+            K.gemm_tn(dy[:, j * C:(j + 1) * C], x, g)
 
 
 # ======================================================================================================================
@@ -516,18 +557,24 @@ class BasicTransformerBlock(nn.Module):
         fg = rt.fg
         df = K.gemm_geglu_bwd(dh3, self.ff.out.wt, sv["f"])  # interleaved d[h | gate]
         if fg is not None:
-            _lin_dw(fg, self.ff.out, dh3, sv["gg"])
-            F2 = df.shape[1]
-            idx = K.geglu_interleave_index(F2 // 2, df.device)
-            tmp = torch.zeros((F2, C), device=df.device, dtype=torch.float32)
-            K.gemm_tn(df, sv["n3"], tmp)
-            fg.g(self.ff.proj.weight).index_add_(0, idx, tmp)
-            tb = torch.zeros((1, F2), device=df.device, dtype=torch.float32)
-            K.colsum_acc(df, tb)
-            fg.g(self.ff.proj.bias).index_add_(0, idx, tb[0])
+            _lin_dw(fg, self.ff.out, dh3, sv["gg"], rt)
+            n3 = sv["n3"]
+
+            def ff_proj_dw():
+                F2 = df.shape[1]
+                idx = K.geglu_interleave_index(F2 // 2, df.device)
+                tmp = torch.zeros((F2, C), device=df.device, dtype=torch.float32)
+                K.gemm_tn(df, n3, tmp)
+                fg.g(self.ff.proj.weight).index_add_(0, idx, tmp)
+                tb = torch.zeros((1, F2), device=df.device, dtype=torch.float32)
+                K.colsum_acc(df, tb)
+                fg.g(self.ff.proj.bias).index_add_(0, idx, tb[0])
+            rt.side.launch(ff_proj_dw, df, n3)
         dn3 = K.gemm(df, self.ff.wt_int)
         if fg is not None:
-            K.layer_norm_dparam(sv["h2"], dn3, sv["st3"], fg.g(self.norm3.weight), fg.g(self.norm3.bias))
+            h2s, st3 = sv["h2"], sv["st3"]
+            rt.side.launch(lambda: K.layer_norm_dparam(h2s, dn3, st3, fg.g(self.norm3.weight), fg.g(self.norm3.bias)),
+                           h2s, dn3, st3)
         dh2 = K.layer_norm_bwd(sv["h2"], dn3, sv["st3"], self.norm3.weight, dadd=dh3)
         # --- cross attention out-proj:  y = a W^T + (a A^T)(sB)^T ;  v = dy sB ; da = dy W + v A ---
         o2 = a2m.to_out[0]
@@ -540,7 +587,7 @@ class BasicTransformerBlock(nn.Module):
         else:
             da2 = K.gemm(dh2, o2.wt)
         if fg is not None:
-            _lin_dw(fg, o2, dh2, sv["a2"])
+            _lin_dw(fg, o2, dh2, sv["a2"], rt)
         enc = rt.enc
         Se = enc.shape[0] // B
         kv3 = sv["kv3"]
@@ -570,10 +617,13 @@ class BasicTransformerBlock(nn.Module):
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         if fg is not None:
-            K.gemm_tn(dq2, sv["n2"], fg.g(a2m.to_q.weight))
-            K.gemm_tn(dkv2[:, :C], enc, fg.g(a2m.to_k.weight))
-            K.gemm_tn(dkv2[:, C:], enc, fg.g(a2m.to_v.weight))
-            K.layer_norm_dparam(sv["h1"], dn2, sv["st2"], fg.g(self.norm2.weight), fg.g(self.norm2.bias))
+            n2, h1s, st2 = sv["n2"], sv["h1"], sv["st2"]
+
+            def attn2_dw():
+                K.gemm_tn(dq2, n2, fg.g(a2m.to_q.weight))
+                _tn_stacked(fg, (a2m.to_k, a2m.to_v), dkv2, enc)
+                K.layer_norm_dparam(h1s, dn2, st2, fg.g(self.norm2.weight), fg.g(self.norm2.bias))
+            rt.side.launch(attn2_dw, dq2, n2, dkv2, enc, h1s, dn2, st2)
         dh1 = K.layer_norm_bwd(sv["h1"], dn2, sv["st2"], self.norm2.weight, dadd=dh2)
         # --- self attention ---
         o1 = a1m.to_out[0]
@@ -586,7 +636,7 @@ class BasicTransformerBlock(nn.Module):
         else:
             da1 = K.gemm(dh1, o1.wt)
         if fg is not None:
-            _lin_dw(fg, o1, dh1, sv["a1"])
+            _lin_dw(fg, o1, dh1, sv["a1"], rt)
         q3 = sv["qkv"].view(B, S, 3 * C)
         dqkv = torch.empty((M, 3 * C), device=dh3.device, dtype=BF16)
         d3 = dqkv.view(B, S, 3 * C)
@@ -610,9 +660,13 @@ class BasicTransformerBlock(nn.Module):
         else:
             dn1 = K.gemm(dqkv, a1m.wt_qkv) if need_dx else None
         if fg is not None:
-            for j, lin in enumerate((a1m.to_q, a1m.to_k, a1m.to_v)):
-                K.gemm_tn(dqkv[:, j * C:(j + 1) * C], sv["n1"], fg.g(lin.weight))
-            K.layer_norm_dparam(sv["x"], dn1, sv["st1"], fg.g(self.norm1.weight), fg.g(self.norm1.bias))
+            n1, xs, st1 = sv["n1"], sv["x"], sv["st1"]
+
+            def attn1_dw():
+                _tn_stacked(fg, (a1m.to_q, a1m.to_k, a1m.to_v), dqkv, n1)
+                if dn1 is not None:
+                    K.layer_norm_dparam(xs, dn1, st1, fg.g(self.norm1.weight), fg.g(self.norm1.bias))
+            rt.side.launch(attn1_dw, dqkv, n1, xs, st1, *((dn1,) if dn1 is not None else ()))
         if not need_dx:  # first adapter block: nothing below it needs a gradient
             return None
         return K.layer_norm_bwd(sv["x"], dn1, sv["st1"], self.norm1.weight, dadd=dh1)
@@ -675,7 +729,7 @@ class Transformer2DModel(nn.Module):
         d2 = dy.view(-1, C)
         fg = rt.fg
         if fg is not None:
-            _lin_dw(fg, self.proj_out, d2, rt.saved.pop()["hout"])
+            _lin_dw(fg, self.proj_out, d2, rt.saved.pop()["hout"], rt)
         dh = K.gemm(d2, self.proj_out.wt)
         for i in reversed(range(len(self.transformer_blocks))):
             dh = self.transformer_blocks[i].bwd(dh, rt.saved.pop(), rt, f"{path}.transformer_blocks.{i}",
@@ -685,7 +739,7 @@ class Transformer2DModel(nn.Module):
             return None
         dn = K.gemm(dh, self.proj_in.wt).view(B, H, W, C)
         if fg is not None:
-            _lin_dw(fg, self.proj_in, dh, sv["xn"])
+            _lin_dw(fg, self.proj_in, dh, sv["xn"], rt)
             return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy,
                                     dgamma=fg.g(self.norm.weight), dbeta=fg.g(self.norm.bias), accumulate=True)
         return K.group_norm_bwd(sv["x"], dn, sv["st"], self.norm.weight, self.norm.bias, False, dadd=dy)
@@ -733,11 +787,11 @@ class ResnetBlock2D(nn.Module):
         B, H, W, _ = dout.shape
         dh2 = K.conv2d(dout, self.conv2.w_dx)
         if fg is not None:
-            _conv_dw(fg, self.conv2, dout.view(-1, self.cout), K.im2col_conv(sv["h2"]))
+            _conv_dw(fg, self.conv2, dout.view(-1, self.cout), sv["h2"], rt, K.im2col_conv)
             dc1 = K.group_norm_bwd(sv["c1"], dh2, sv["st2"], self.norm2.weight, self.norm2.bias, True,
                                    dgamma=fg.g(self.norm2.weight), dbeta=fg.g(self.norm2.bias), accumulate=True)
             dc2 = dc1.view(-1, self.cout)
-            _conv_dw(fg, self.conv1, dc2, K.im2col_conv(sv["h1"]))
+            _conv_dw(fg, self.conv1, dc2, sv["h1"], rt, K.im2col_conv)
             # time-embedding row bias (one row per image): per-image column sums -> the time_emb_proj output grad
             K.colsum_acc(dc2, rt.dtemb[:, self._temb_off:self._temb_off + self.cout], rows_per_group=H * W)
         else:
@@ -746,9 +800,13 @@ class ResnetBlock2D(nn.Module):
         if self.conv_shortcut is not None:
             dsc = K.gemm(dout.view(-1, self.cout), self.conv_shortcut.wt).view(B, H, W, self.cin)
             if fg is not None:
-                K.gemm_tn(dout.view(-1, self.cout), sv["x"].view(-1, self.cin),
-                          fg.g(self.conv_shortcut.weight).view(self.cout, self.cin))
-                K.colsum_acc(dout.view(-1, self.cout), fg.g(self.conv_shortcut.bias).view(1, -1))
+                d2, x2 = dout.view(-1, self.cout), sv["x"].view(-1, self.cin)
+                sc = self.conv_shortcut
+
+                def sc_dw():
+                    K.gemm_tn(d2, x2, fg.g(sc.weight).view(self.cout, self.cin))
+                    K.colsum_acc(d2, fg.g(sc.bias).view(1, -1))
+                rt.side.launch(sc_dw, d2, x2)
         else:
             dsc = dout
         if fg is not None:
@@ -773,7 +831,8 @@ class Downsample2D(nn.Module):
     def bwd(self, dy, rt):
         sv = rt.saved.pop()
         if rt.fg is not None:
-            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout), K.im2col_conv(sv["x"], stride=2))
+            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout), sv["x"], rt,
+                     lambda x: K.im2col_conv(x, stride=2))
         return K.conv2d(dy, self.conv.w_dx, mode=K.CONV_T2, out_hw=tuple(sv["hw"]))
 
 
@@ -792,8 +851,8 @@ class Upsample2D(nn.Module):
 
     def bwd(self, dy, rt):
         if rt.fg is not None:
-            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout),
-                     K.im2col_conv(rt.saved.pop()["x"], mode=K.CONV_UP2))
+            _conv_dw(rt.fg, self.conv, dy.reshape(-1, self.conv.cout), rt.saved.pop()["x"], rt,
+                     lambda x: K.im2col_conv(x, mode=K.CONV_UP2))
         du = K.conv2d(dy, self.conv.w_dx)  # input-gradient on the 2x grid
         return K.sumpool2(du)
 
@@ -1142,8 +1201,11 @@ class UNet2DConditionModel(nn.Module):
 
     # ---------------- forward / backward ----------------
     def _runtime(self, B, enc, save, lora_on):
-        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=K.SideStream(),
-                             fg=self.full if save else None)
+        fg = self.full if save else None
+        # full-UNet weight gradients run on the side stream beside the input-gradient GEMMs they do not feed (the
+        # small-M dX and dW products each leave most CUs idle; GradBuckets joins it before each bucket's all-reduce)
+        side = K.SideStream(enabled=True) if (fg is not None and _FULL_SIDE) else K.SideStream()
+        rt = SimpleNamespace(B=B, enc=enc, save=save, saved=[], lora_on=lora_on, paired=False, side=side, fg=fg)
         rt.pol = lambda t: t[:t.shape[0] // 2] if rt.paired else t
         rt.kv_cache = {}
         rt.kv_text = lambda C: self.kv_text(rt, C)
@@ -1263,7 +1325,7 @@ class UNet2DConditionModel(nn.Module):
             co = self.conv_out.cout
             dy8 = torch.zeros((B * H * W, 8), device=dout.device, dtype=BF16)  # TN operands need 8 | width
             dy8[:, :co] = dout.reshape(-1, co)
-            _conv_dw(fg, self.conv_out, dy8, K.im2col_conv(sv["hn"]))
+            _conv_dw(fg, self.conv_out, dy8, sv["hn"], rt, K.im2col_conv)
             dh = K.group_norm_bwd(sv["h"], dhn, sv["st"], self.conv_norm_out.weight, self.conv_norm_out.bias, True,
                                   dgamma=fg.g(self.conv_norm_out.weight), dbeta=fg.g(self.conv_norm_out.bias),
                                   accumulate=True)

@@ -127,7 +127,9 @@ def test_grad_units_tile_the_flat_gradient(full):
     if full:
         fg = unet.enable_full_grads()
         n = fg.numel
-        assert n == sum(p.numel() for p in unet.parameters())
+        slot = lambda k: -(-k // fg.ALIGN) * fg.ALIGN  # every tensor on a 64-element slot boundary
+        assert n == sum(slot(p.numel()) for p in unet.parameters())
+        assert all(off % fg.ALIGN == 0 for off, _ in fg.offsets.values())
     else:
         st = unet.add_adapter(SimpleNamespace(r=8, lora_alpha=8))
         n = st.numel

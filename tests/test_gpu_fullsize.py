@@ -253,7 +253,7 @@ def test_c3_dmd_full_unet_window_at_1024(cuda, P):
         gp = torch.Generator(device="cuda").manual_seed(7)
         for p in unet.parameters():
             p.add_((torch.randn(p.shape, device=cuda, generator=gp) * 2e-3 * p.float().abs().mean()).bfloat16())
-        fg.master.copy_(torch.cat([p.detach().float().reshape(-1) for p in fg.params]))
+        fg.master_from_params()
     unet.prepare()
     tr = PSOTrainer(unet, mode="dmd", num_steps=N, gradient_accumulation_steps=gas, train_batch_size=P,
                     ref_unet=ref_unet)

@@ -136,16 +136,24 @@ def test_conv_stride1_input_grad_flipped(cuda):
                                    # full-weight gradients (128 x 128 TN tiles): ragged M / I / J, split-K atomics
                                    (16384, 1280, 1280), (1000, 640, 320), (616, 2880, 640), (77, 136, 264),
                                    (16384, 128, 128), (4100, 1152, 320)])
-def test_gemm_tn_vs_fp32(cuda, M, I, J):
-    """Generic TN path and the streaming rank-r path (one side 32 / 64 / 96 wide), partial 64-row steps included."""
+@pytest.mark.parametrize("split_ws", [True, False])
+def test_gemm_tn_vs_fp32(cuda, M, I, J, split_ws):
+    """Generic TN path and the streaming rank-r path (one side 32 / 64 / 96 wide), partial 64-row steps included;
+    full-weight shapes with few 128 x 128 tiles through the workspace split (pso_gemm_tn_ws: partial products stored
+    per row slice, added in slice order) and, split_ws=False, through pso_gemm_tn (f32-atomic split)."""
     from pairwise_sample_optimization_amd import kernels as K_
     big = torch.randn(M, I + 16, device=cuda).bfloat16()
     a = big[:, 8:8 + I]          # column-slice view (row stride != I)
     b = torch.randn(M, J, device=cuda).bfloat16()
     out = torch.randn(I, J, device=cuda)
     ref = out + 0.5 * (a.float().t() @ b.float())
-    K_.gemm_tn(a, b, out, alpha=0.5)
+    K_.gemm_tn(a, b, out, alpha=0.5, split_ws=split_ws)
     assert _rel(out, ref) < 1e-5
+    if split_ws and K_.lib().pso_gemm_tn_ws_bytes(M, I, J):  # the ordered reduction is deterministic
+        o1, o2 = torch.zeros(I, J, device=cuda), torch.zeros(I, J, device=cuda)
+        K_.gemm_tn(a, b, o1)
+        K_.gemm_tn(a, b, o2)
+        assert torch.equal(o1, o2)
 
 
 @pytest.mark.parametrize("M,C,G", [(8192, 1280, 3), (1000, 640, 3), (616, 1280, 2)])
@@ -537,10 +545,13 @@ def test_tn_rank_batch_equals_individual_products(cuda):
         assert ((o2 - ref).norm() / ref.norm()).item() < 1e-3, (M, I, J, grp)
 
 
-def test_adamw8bit_vs_restatement(cuda):
+@pytest.mark.parametrize("n", [2048 * 37, 2048 * 5 + 1003])
+def test_adamw8bit_vs_restatement(cuda, n):
     """pso_adamw8bit_step (bitsandbytes AdamW8bit, the reference's default optimizer T:427-435) against the numpy
     restatement oracle/adam8bit.py over 5 steps from zero state: the maps are the same floats, every quantised code and
-    block absmax agrees, parameters to fp32 rounding (parity unpinned: no bitsandbytes here)."""
+    block absmax agrees, parameters to fp32 rounding (parity unpinned: no bitsandbytes here).  The ragged size checks
+    the kernel's scalar tail (partial last block and thread) against the restatement on the zero-padded vector (padded
+    elements keep m = v = 0 and do not move a block's absmax)."""
     import numpy as np
     import ctypes
     from oracle import adam8bit as O
@@ -550,23 +561,25 @@ def test_adamw8bit_vs_restatement(cuda):
     K_.lib().pso_adamw8bit_maps(s, u)
     assert np.array_equal(np.array(list(s), dtype=np.float32), O.create_dynamic_map(True))
     assert np.array_equal(np.array(list(u), dtype=np.float32), O.create_dynamic_map(False))
-    n = 2048 * 37
+    npad = -(-n // 2048) * 2048
     g_ = np.random.default_rng(3)
-    p = g_.standard_normal(n).astype(np.float32) * 0.02
+    p = np.zeros(npad, np.float32)
+    p[:n] = g_.standard_normal(n).astype(np.float32) * 0.02
     f32 = lambda x: float(np.float32(x))
     lr, b1, b2, eps, wd = f32(1e-3), f32(0.9), f32(0.999), f32(1e-8), f32(1e-2)
-    pd = torch.tensor(p, device=cuda)
+    pd = torch.tensor(p[:n], device=cuda)
     st = K_.Adam8State(n, cuda)
-    qm, qv = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
-    am, av = np.zeros(n // 2048, np.float32), np.zeros(n // 2048, np.float32)
+    qm, qv = np.zeros(npad, np.uint8), np.zeros(npad, np.uint8)
+    am, av = np.zeros(npad // 2048, np.float32), np.zeros(npad // 2048, np.float32)
     for step in range(1, 6):
-        gr = (g_.standard_normal(n) * np.exp(g_.standard_normal(n))).astype(np.float32) * 1e-2
-        K_.adamw8bit_step(pd, torch.tensor(gr, device=cuda), st, lr, (b1, b2), eps, wd, step)
+        gr = np.zeros(npad, np.float32)
+        gr[:n] = (g_.standard_normal(n) * np.exp(g_.standard_normal(n))).astype(np.float32) * 1e-2
+        K_.adamw8bit_step(pd, torch.tensor(gr[:n], device=cuda), st, lr, (b1, b2), eps, wd, step)
         p, qm, qv, am, av = O.adamw8bit_step(p, gr, qm, qv, am, av, lr, b1, b2, eps, wd, step)
     torch.cuda.synchronize()
     assert np.array_equal(st.am.cpu().numpy(), am) and np.array_equal(st.av.cpu().numpy(), av)
-    assert (st.qm.cpu().numpy() == qm).mean() > 0.9999 and (st.qv.cpu().numpy() == qv).mean() > 0.9999
-    assert np.abs(pd.cpu().numpy() - p).max() <= 1e-6 * np.abs(p).max()
+    assert (st.qm.cpu().numpy() == qm[:n]).mean() > 0.9999 and (st.qv.cpu().numpy() == qv[:n]).mean() > 0.9999
+    assert np.abs(pd.cpu().numpy() - p[:n]).max() <= 1e-6 * np.abs(p).max()
     # it is an Adam step: against fp32 AdamW the parameters move the same way (codes cost a few % of the update)
     m, v = st.dequant()
     assert torch.isfinite(m).all() and (v >= 0).all()

@@ -21,18 +21,24 @@ def test_group_norm_fwd_bwd(cuda, B, HW, C, silu):
     gm = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
     bt = (0.1 * torch.randn(C, device=cuda)).bfloat16()
     xr = x.float().permute(0, 2, 1).requires_grad_(True)  # [B,C,HW]
-    ref = F.group_norm(xr, 32, gm.float(), bt.float(), eps=1e-5)
+    gmr, btr = gm.float().requires_grad_(True), bt.float().requires_grad_(True)
+    ref = F.group_norm(xr, 32, gmr, btr, eps=1e-5)
     if silu:
         ref = F.silu(ref)
     y, st = K.group_norm_fwd(x, gm, bt, 32, 1e-5, silu)
     assert _rel(y.permute(0, 2, 1), ref) < 8e-3
     dy = torch.randn_like(y)
-    (gx,) = torch.autograd.grad(ref, xr, dy.float().permute(0, 2, 1))
+    gx, ggm, gbt = torch.autograd.grad(ref, (xr, gmr, btr), dy.float().permute(0, 2, 1))
     dadd = torch.randn_like(x)
     dg = torch.zeros(C, device=cuda)
     db = torch.zeros(C, device=cuda)
     dx = K.group_norm_bwd(x, dy, st, gm, bt, silu, dadd=dadd, dgamma=dg, dbeta=db)
     assert _rel(dx.permute(0, 2, 1), gx + dadd.float().permute(0, 2, 1)) < 1e-2
+    # dgamma / dbeta (the full-UNet weight gradients; split reduction when B * HW / 64 >= 4)
+    assert _rel(dg, ggm) < 1e-2 and _rel(db, gbt) < 1e-2
+    dg2, db2 = dg.clone(), db.clone()
+    K.group_norm_bwd(x, dy, st, gm, bt, silu, dadd=dadd, dgamma=dg2, dbeta=db2, accumulate=True)
+    assert _rel(dg2, 2 * ggm) < 1e-2 and _rel(db2, 2 * gbt) < 1e-2
 
 
 @pytest.mark.parametrize("M,C", [(300, 640), (77, 1280), (1024, 320), (64, 2048)])

@@ -22,7 +22,7 @@ def main():
     bench.one_step(tr, buf, g)
     torch.cuda.synchronize()
     K.PROFILE = []
-    K.SideStream.enabled = False  # serial launches so every event pair times one kernel
+    K.SideStream.enabled_any = False  # serial launches so every event pair times one kernel
     bench.one_step(tr, buf, g)
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
