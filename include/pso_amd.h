@@ -375,6 +375,12 @@ void pso_adamw8bit_maps(float* signed_map, float* unsigned_map);
 int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
                        float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
                        float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream);
+/* The same step that also writes the updated parameters rounded to bf16 (RNE) into param_bf16 [n] (16-B aligned; NULL
+ * = pso_adamw8bit_step): the bf16 working copy the UNet kernels read, without a separate cast pass. */
+int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q,
+                            uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v, float lr, float beta1, float beta2,
+                            float eps, float weight_decay, int step, float grad_scale, const float* clip_coef,
+                            void* stream);
 int pso_zero_f32(long n, float* x, void* stream);
 int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
                    void* stream);

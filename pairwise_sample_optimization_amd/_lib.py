@@ -113,6 +113,7 @@ SIGNATURES = {
     "pso_adamw8bit_blocks": (csz, [cl]),
     "pso_adamw8bit_maps": (None, [vp, vp]),
     "pso_adamw8bit_step": (ci, [cl, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
+    "pso_adamw8bit_step_bf16": (ci, [cl, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
     "pso_zero_f32": (ci, [cl, vp, vp]),
     "pso_preference": (ci, [ci, ci, vp, vp, ci, vp, vp]),
     "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),

@@ -95,16 +95,24 @@ __global__ void timestep_embed_kernel(int n, int dim, const float* __restrict__ 
 }
 
 // 64x64 tiled transpose, bf16: in [R][C] (ldi) -> out [C][Rp] (ldo); rows R..Rp-1 of the input read as zero
-__global__ void transpose_kernel(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
-                                 bf16_t* __restrict__ out, long ldo) {
-  __shared__ bf16_t tile[64][66];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
-  for (int i = ty; i < 64; i += 4) {
-    const int r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < R && c < C) ? in[(long)r * ldi + c] : (bf16_t)0;
+__global__ __launch_bounds__(256) void transpose_kernel(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
+                                                        bf16_t* __restrict__ out, long ldo) {
+  // 64 x 64 tile: rows read as 16-B chunks where the view allows (C, ldi multiples of 8, 16-B base), written back as
+  // 64 consecutive 2-B elements per output row
+  __shared__ bf16_t tile[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64, t = threadIdx.x;
+  const bool vec = (C % 8) == 0 && (ldi % 8) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  for (int q = t; q < 64 * 8; q += 256) {
+    const int i = q >> 3, c = (q & 7) * 8, r = r0 + i;
+    const bf16_t* src = in + (long)r * ldi + c0 + c;
+    if (vec && r < R && c0 + c + 8 <= C) {
+      *reinterpret_cast<uint4*>(&tile[i][c]) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      for (int e = 0; e < 8; ++e) tile[i][c + e] = (r < R && c0 + c + e < C) ? src[e] : (bf16_t)0;
+    }
   }
   __syncthreads();
+  const int tx = t & 63, ty = t >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int c = c0 + i, r = r0 + tx;
     if (c < C && r < Rp) out[(long)c * ldo + r] = tile[tx][i];
@@ -175,25 +183,61 @@ __global__ void axpby_kernel(long n8, float a, const bf16_t* __restrict__ x, flo
   }
 }
 
+// casts: 8 elements per thread (32-B / 16-B accesses) where both buffers are 16-B aligned, scalar otherwise and for
+// the ragged tail
 __global__ void cast_f32_bf16_kernel(long n, const float* __restrict__ x, float scale, bf16_t* __restrict__ y) {
-  GRID_STRIDE(i, n) y[i] = f2bf(x[i] * scale);
+  long done = 0;
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+    done = n & ~7L;
+    GRID_STRIDE(v, n >> 3) {
+      const float4 a = reinterpret_cast<const float4*>(x)[2 * v], b = reinterpret_cast<const float4*>(x)[2 * v + 1];
+      reinterpret_cast<uint4*>(y)[v] = make_uint4(pack2bf(a.x * scale, a.y * scale), pack2bf(a.z * scale, a.w * scale),
+                                                  pack2bf(b.x * scale, b.y * scale), pack2bf(b.z * scale, b.w * scale));
+    }
+  }
+  GRID_STRIDE(i, n - done) y[done + i] = f2bf(x[done + i] * scale);
 }
 __global__ void cast_bf16_f32_kernel(long n, const bf16_t* __restrict__ x, float* __restrict__ y) {
-  GRID_STRIDE(i, n) y[i] = bf2f(x[i]);
+  long done = 0;
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+    done = n & ~7L;
+    GRID_STRIDE(v, n >> 3) {
+      const uint4 u = reinterpret_cast<const uint4*>(x)[v];
+      reinterpret_cast<float4*>(y)[2 * v] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      reinterpret_cast<float4*>(y)[2 * v + 1] = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                                            __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u));
+    }
+  }
+  GRID_STRIDE(i, n - done) y[done + i] = bf2f(x[done + i]);
 }
 
-// conv weight [Co][kh][kw][Ci] -> input-gradient weight [Ci][kh'][kw'][Co]; flip=1: kh'=ks-1-kh (stride-1 bwd)
-__global__ void conv_weight_t_kernel(int Co, int ks, int Ci, int flip, const bf16_t* __restrict__ w,
-                                     bf16_t* __restrict__ wt) {
-  GRID_STRIDE(i, (long)Co * ks * ks * Ci) {
-    const int ci = (int)(i % Ci);
-    long r = i / Ci;
-    const int kw = (int)(r % ks);
-    r /= ks;
-    const int kh = (int)(r % ks);
-    const int co = (int)(r / ks);
-    const int kh2 = flip ? ks - 1 - kh : kh, kw2 = flip ? ks - 1 - kw : kw;
-    wt[(((long)ci * ks + kh2) * ks + kw2) * Co + co] = w[i];
+// conv weight [Co][kh][kw][Ci] -> input-gradient weight [Ci][kh'][kw'][Co]; flip=1: kh'=ks-1-kh (stride-1 bwd).
+// Per tap this is a [Co][Ci] -> [Ci][Co] transpose of a strided view: 64 x 64 tiles through LDS, one tap per
+// blockIdx.z, 16-B reads along Ci and 2-B writes along Co by 64 consecutive lanes (was one scattered 2-B store per
+// element, Co elements apart).
+__global__ __launch_bounds__(256) void conv_weight_t_kernel(int Co, int ks, int Ci, int flip,
+                                                            const bf16_t* __restrict__ w, bf16_t* __restrict__ wt) {
+  __shared__ bf16_t tile[64][72];  // [co][ci], 144-B pitch
+  const int tap = blockIdx.z, kh = tap / ks, kw = tap - kh * ks;
+  const int tap2 = flip ? (ks - 1 - kh) * ks + (ks - 1 - kw) : tap;
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, t = threadIdx.x;
+  const long ldw = (long)ks * ks * Ci;
+  const bool vec = (Ci % 8) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
+  for (int q = t; q < 64 * 8; q += 256) {  // 64 rows (co) x 8 chunks of 8 ci
+    const int r = q >> 3, c = (q & 7) * 8, co = co0 + r, ci = ci0 + c;
+    const bf16_t* src = w + co * ldw + (long)tap * Ci + ci;
+    if (vec && co < Co && ci + 8 <= Ci) {
+      *reinterpret_cast<uint4*>(&tile[r][c]) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      for (int e = 0; e < 8; ++e) tile[r][c + e] = (co < Co && ci + e < Ci) ? src[e] : (bf16_t)0;
+    }
+  }
+  __syncthreads();
+  const int lx = t & 63, ly = t >> 6;
+  for (int i = ly; i < 64; i += 4) {  // output row ci0 + i, 64 consecutive co
+    const int ci = ci0 + i, co = co0 + lx;
+    if (ci < Ci && co < Co) wt[((long)ci * ks * ks + tap2) * Co + co] = tile[lx][i];
   }
 }
 
@@ -446,17 +490,17 @@ int pso_axpby(long n, float a, const void* x, float b, const void* z, void* y, v
 }
 
 int pso_cast_f32_bf16(long n, const float* x, float scale, void* y, void* stream) {
-  cast_f32_bf16_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(n, x, scale, (bf16_t*)y);
+  cast_f32_bf16_kernel<<<grid_for(n, 8), 256, 0, (hipStream_t)stream>>>(n, x, scale, (bf16_t*)y);
   return pso_check_launch("pso_cast_f32_bf16");
 }
 
 int pso_cast_bf16_f32(long n, const void* x, float* y, void* stream) {
-  cast_bf16_f32_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(n, (const bf16_t*)x, y);
+  cast_bf16_f32_kernel<<<grid_for(n, 8), 256, 0, (hipStream_t)stream>>>(n, (const bf16_t*)x, y);
   return pso_check_launch("pso_cast_bf16_f32");
 }
 
 int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt, void* stream) {
-  conv_weight_t_kernel<<<grid_for((long)Co * ks * ks * Ci), 256, 0, (hipStream_t)stream>>>(
+  conv_weight_t_kernel<<<dim3(cdiv(Ci, 64), cdiv(Co, 64), ks * ks), 256, 0, (hipStream_t)stream>>>(
       Co, ks, Ci, flip, (const bf16_t*)w, (bf16_t*)wt);
   return pso_check_launch("pso_conv_weight_t");
 }

@@ -16,11 +16,22 @@
 
 #define OPT_THREADS 256
 
-// partial sums of g^2 (fp64) per block -> one final block computes the clip coefficient
+// partial sums of g^2 (fp64) per block -> one final block computes the clip coefficient.  16-B loads where the
+// gradient is 16-B aligned (the flat buckets are), the ragged tail by the scalar loop.
 __global__ void sqnorm_partial_kernel(long n, const float* __restrict__ g, double* __restrict__ part) {
   __shared__ double red[OPT_THREADS / 64];
   double acc = 0.0;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x, nth = (long)gridDim.x * blockDim.x;
+  long tail = 0;
+  if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    const long n4 = n >> 2;
+    for (long i = tid; i < n4; i += nth) {
+      const float4 v = reinterpret_cast<const float4*>(g)[i];
+      acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    tail = n4 << 2;
+  }
+  for (long i = tail + tid; i < n; i += nth) {
     const double v = g[i];
     acc += v * v;
   }
@@ -88,25 +99,36 @@ struct Adam8Maps {
   float s[256], u[256];
 };
 
-// nearest code of x in a sorted 256-entry map (ties -> the lower index): the count of entries below x by a branch-free
-// 8-step search (equal to lower_bound except that it stops at 255, which the clamp below maps to the same index), then
-// the nearer neighbour.  The searches of a thread's 16 values run in lockstep (adam8_nearest16), so every step issues
-// 16 independent LDS reads instead of one dependent chain per value.
+// nearest code of x in a sorted 256-entry map (ties -> the lower index): lo = the count of the first 255 entries
+// below x (equal to lower_bound except that it stops at 255, which the clamp below maps to the same index), then the
+// nearer neighbour.  The count descends a breadth-first (Eytzinger) copy of those 255 entries, tree[1..255]: step d
+// reads one of the 2^d consecutive nodes of level d, so the 64 lanes' reads of a level hit distinct LDS banks (the
+// sorted-order bisection probed entries 2h apart at step h -- one bank for every lane -- and serialised up to 4-way).
+// The searches of a thread's values run in lockstep, so every level issues NV independent LDS reads.
 template <int NV>
-__device__ __forceinline__ void adam8_nearest16(const float* __restrict__ code, const float (&x)[NV], int (&idx)[NV]) {
-  int lo[NV];
+__device__ __forceinline__ void adam8_nearest(const float* __restrict__ code, const float* __restrict__ tree,
+                                              const float (&x)[NV], int (&idx)[NV]) {
+  int nd[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) lo[k] = 0;
+  for (int k = 0; k < NV; ++k) nd[k] = 1;
 #pragma unroll
-  for (int h = 128; h > 0; h >>= 1)
+  for (int d = 0; d < 8; ++d)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) lo[k] += code[lo[k] + h - 1] < x[k] ? h : 0;
+    for (int k = 0; k < NV; ++k) nd[k] = 2 * nd[k] + (tree[nd[k]] < x[k] ? 1 : 0);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int i = lo[k] < 1 ? 1 : lo[k];
+    const int lo = nd[k] - 256;
+    const int i = lo < 1 ? 1 : lo;
     const float a = code[i - 1], b = code[i];
     idx[k] = fabsf(x[k] - a) <= fabsf(b - x[k]) ? i - 1 : i;
   }
+}
+
+// node of the breadth-first tree over sorted entries 0..254 that holds sorted entry i: height h = ctz(i + 1) above
+// the leaves, position (i + 1) >> (h + 1) within its level
+__device__ __forceinline__ int adam8_node(int i) {
+  const int h = __builtin_ctz(i + 1);
+  return (1 << (7 - h)) + ((i + 1) >> (h + 1));
 }
 
 __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
@@ -114,13 +136,17 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
                                                         float* __restrict__ am, float* __restrict__ av, float b1,
                                                         float omb1, float b2, float omb2, float eps_c2, float step_size,
                                                         float decay, float gscale, const float* __restrict__ clip,
-                                                        Adam8Maps maps) {
+                                                        bf16_t* __restrict__ pw, Adam8Maps maps) {
 #pragma clang fp contract(off)
-  __shared__ float cs[256], cu[256];
+  __shared__ float cs[256], cu[256], ts[256], tu[256];
   __shared__ float red[2][4];
   const int t = threadIdx.x;
   cs[t] = maps.s[t];
   cu[t] = maps.u[t];
+  if (t < 255) {
+    ts[adam8_node(t)] = maps.s[t];
+    tu[adam8_node(t)] = maps.u[t];
+  }
   const long blk = blockIdx.x;
   const long i0 = blk * ADAM8_BLOCK + (long)t * 8;
   const bool full = i0 + 8 <= n;  // every thread of a block but the last block's tail: 32-B / 8-B vector accesses
@@ -184,11 +210,15 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
     xv[e] = nv > 0.f ? v[e] / nv : 0.f;
   }
   int im[8], iv[8];
-  adam8_nearest16(cs, xm, im);
-  adam8_nearest16(cu, xv, iv);
+  adam8_nearest(cs, ts, xm, im);
+  adam8_nearest(cu, tu, xv, iv);
   if (full) {
     *reinterpret_cast<float4*>(p + i0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
     *reinterpret_cast<float4*>(p + i0 + 4) = make_float4(pv[4], pv[5], pv[6], pv[7]);
+    if (pw) {  // the bf16 working copy of the parameters (round to nearest even), 16-B store
+      *reinterpret_cast<uint4*>(pw + i0) =
+          make_uint4(pack2bf(pv[0], pv[1]), pack2bf(pv[2], pv[3]), pack2bf(pv[4], pv[5]), pack2bf(pv[6], pv[7]));
+    }
     *reinterpret_cast<uint2*>(qm + i0) =
         make_uint2((uint32_t)im[0] | (uint32_t)im[1] << 8 | (uint32_t)im[2] << 16 | (uint32_t)im[3] << 24,
                    (uint32_t)im[4] | (uint32_t)im[5] << 8 | (uint32_t)im[6] << 16 | (uint32_t)im[7] << 24);
@@ -201,6 +231,7 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
       const long i = i0 + e;
       if (i >= n) continue;
       p[i] = pv[e];
+      if (pw) pw[i] = f2bf(pv[e]);
       qm[i] = (uint8_t)im[e];
       qv[i] = (uint8_t)iv[e];
     }
@@ -302,13 +333,13 @@ void pso_adamw8bit_maps(float* signed_map, float* unsigned_map) {
   adam8_dynamic_map(false, unsigned_map);
 }
 
-int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
+int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
                        float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
                        float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
   PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0,
-                "pso_adamw8bit_step: bad args");
-  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
-                "pso_adamw8bit_step: param / grad need 16-B, the code arrays 8-B alignment");
+                "pso_adamw8bit_step_bf16: bad args");
+  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
+                "pso_adamw8bit_step_bf16: param / grad / param_bf16 need 16-B, the code arrays 8-B alignment");
   static Adam8Maps maps = [] {
     Adam8Maps m;
     adam8_dynamic_map(true, m.s);
@@ -323,8 +354,16 @@ int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg
   const int nb = (int)pso_adamw8bit_blocks(n);
   adamw8bit_kernel<<<nb, 256, 0, (hipStream_t)stream>>>(n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v,
                                                          beta1, (float)(1.0 - b1), beta2, (float)(1.0 - b2),
-                                                         c2 * eps, step_size, decay, grad_scale, clip_coef, maps);
-  return pso_check_launch("pso_adamw8bit_step");
+                                                         c2 * eps, step_size, decay, grad_scale, clip_coef,
+                                                         (bf16_t*)param_bf16, maps);
+  return pso_check_launch("pso_adamw8bit_step_bf16");
+}
+
+int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
+                       float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
+  return pso_adamw8bit_step_bf16(n, param, nullptr, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, lr, beta1,
+                                 beta2, eps, weight_decay, step, grad_scale, clip_coef, stream);
 }
 
 int pso_zero_f32(long n, float* x, void* stream) {

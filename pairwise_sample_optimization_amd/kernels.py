@@ -769,12 +769,17 @@ class Adam8State:
         return cs[self.qm.long()] * self.am[blk], cu[self.qv.long()] * self.av[blk]
 
 
-def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None):
+def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None, out_bf16=None):
+    """One 8-bit AdamW step on the flat fp32 param; out_bf16 (same numel, bf16) also receives the updated parameters
+    rounded to bf16 (the working copy), in the same pass."""
     require_cuda(param, grad)
-    check(lib().pso_adamw8bit_step(param.numel(), ptr(param), ptr(grad), ptr(state.qm), ptr(state.qv), ptr(state.am),
-                                   ptr(state.av), float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                   float(weight_decay), int(step), float(grad_scale), ptr(clip), stream_ptr()),
-          "pso_adamw8bit_step")
+    if out_bf16 is not None:
+        assert out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == param.numel() and out_bf16.is_contiguous()
+    check(lib().pso_adamw8bit_step_bf16(param.numel(), ptr(param), ptr(out_bf16), ptr(grad), ptr(state.qm),
+                                        ptr(state.qv), ptr(state.am), ptr(state.av), float(lr), float(betas[0]),
+                                        float(betas[1]), float(eps), float(weight_decay), int(step), float(grad_scale),
+                                        ptr(clip), stream_ptr()),
+          "pso_adamw8bit_step_bf16")
 
 
 def zero_(x):

@@ -205,11 +205,20 @@ class GradBuckets:
 
 def trainable(unet):
     """(master, grad, refresh) of what the step trains: the flat LoRA bucket (the reference's recipe), or every UNet
-    parameter when unet.enable_full_grads() was called (BASELINE C3 / C4, build-only)."""
+    parameter when unet.enable_full_grads() was called (BASELINE C3 / C4, build-only).  refresh(cast=True)."""
     if getattr(unet, "full", None) is not None:
         return unet.full.master, unet.full.grad, unet.refresh_full
     st = unet.lora
     return st.master, st.grad, st.refresh
+
+
+def _work_copy(unet, master):
+    """The flat bf16 working copy that refresh() casts the master into (the optimizer can write it directly)."""
+    st = unet.full if getattr(unet, "full", None) is not None else unet.lora
+    w = getattr(st, "work", None)
+    ok = (w is not None and w.dtype == torch.bfloat16 and w.numel() == master.numel() and w.is_contiguous()
+          and w.data_ptr() % 16 == 0)
+    return w if ok else None
 
 
 def lora_optimizer_step(tr):
@@ -226,14 +235,17 @@ def lora_optimizer_step(tr):
         scale = allreduce_grads(grad, tr.pg, getattr(tr, "allreduce_dtype", None))
     K.grad_clip_coef(grad, tr.max_grad_norm, grad_scale=scale, out=tr.clip_buf)
     tr.opt_step += 1
+    cast = True
     if getattr(tr, "adam8", None) is not None:  # train.use_8bit_adam: bitsandbytes AdamW8bit (T:427-435)
+        work = _work_copy(tr.unet, master)  # the step also writes the bf16 working copy (no separate cast pass)
         K.adamw8bit_step(master, grad, tr.adam8, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
-                         grad_scale=scale, clip=tr.clip_buf)
+                         grad_scale=scale, clip=tr.clip_buf, out_bf16=work)
+        cast = work is None
     else:
         K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
                      grad_scale=scale, clip=tr.clip_buf)
     K.zero_(grad)
-    refresh()
+    refresh(cast=cast)
 
 
 class PSOTrainer:

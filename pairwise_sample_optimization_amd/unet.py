@@ -150,6 +150,22 @@ class Norm(nn.Module):
             self.bias.zero_()
 
 
+def _stacked(ws):
+    """torch.cat(ws, 0) of same-width row-major weights -- as a zero-copy view when they already lie back to back in
+    memory (the full-UNet flat working copy keeps a block's q/k/v, and k/v, adjacent), else a new tensor."""
+    w0 = ws[0]
+    adjacent = all(w.is_contiguous() and w.dtype == w0.dtype and w.shape[1:] == w0.shape[1:] for w in ws)
+    if adjacent:
+        off = w0.data_ptr()
+        for w in ws:
+            adjacent = adjacent and w.data_ptr() == off
+            off += w.numel() * w.element_size()
+    if adjacent:
+        rows = sum(w.shape[0] for w in ws)
+        return torch.as_strided(w0, (rows,) + tuple(w0.shape[1:]), w0.stride())
+    return torch.cat(ws, 0)
+
+
 # ======================================================================================================================
 # Full-UNet training state (BASELINE C3 / C4, SURVEY §8a a6 "full dW in C3 (build-only)")
 # ======================================================================================================================
@@ -212,10 +228,12 @@ class FullGradState:
         with torch.no_grad():
             K.cast_bf16_f32(self.work, out=self.master)
 
-    def refresh(self):
-        """master -> bf16 module weights (the caller re-runs prepare()): one cast over the flat buffers."""
-        with torch.no_grad():
-            K.cast_f32_bf16(self.master, out=self.work)
+    def refresh(self, cast=True):
+        """master -> bf16 module weights (the caller re-runs prepare()): one cast over the flat buffers (cast=False:
+        the optimizer already wrote them)."""
+        if cast:
+            with torch.no_grad():
+                K.cast_f32_bf16(self.master, out=self.work)
 
 
 _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
@@ -374,10 +392,12 @@ class LoraState:
                 B.zero_()
         self.refresh()
 
-    def refresh(self):
-        """bf16 working copies (B pre-scaled by alpha/r) and their transposed forms after a master update."""
+    def refresh(self, cast=True):
+        """bf16 working copies (B pre-scaled by alpha/r) and their transposed forms after a master update (cast=False:
+        the optimizer already wrote work = bf16(master))."""
         self.version = getattr(self, "version", 0) + 1  # keys the fp8 copies of the sB stacks (fp8 forward)
-        K.cast_f32_bf16(self.master, out=self.work)
+        if cast:
+            K.cast_f32_bf16(self.master, out=self.work)
         if self.scale != 1.0:
             for Bw in self._b_views:
                 K.axpby(self.scale, Bw, out=Bw)
@@ -431,10 +451,10 @@ class Attention(nn.Module):
     def prepare(self, self_attn):
         C = self.dim
         if self_attn:
-            self.w_qkv = torch.cat([self.to_q.weight.data, self.to_k.weight.data, self.to_v.weight.data], 0)
+            self.w_qkv = _stacked([self.to_q.weight.data, self.to_k.weight.data, self.to_v.weight.data])
             self.wt_qkv = K.transpose(self.w_qkv)  # [C][3C]
         else:
-            self.w_kv = torch.cat([self.to_k.weight.data, self.to_v.weight.data], 0)
+            self.w_kv = _stacked([self.to_k.weight.data, self.to_v.weight.data])
             self.to_q.prepare()
         self.to_out[0].prepare()
 
@@ -1058,8 +1078,11 @@ class UNet2DConditionModel(nn.Module):
                 if hasattr(blk, "attentions"):
                     units.append((f"down_blocks.{i}.attentions.{j}", under(f"down_blocks.{i}.attentions.{j}")))
                 units.append((f"down_blocks.{i}.resnets.{j}", under(f"down_blocks.{i}.resnets.{j}")))
-        units.append(("embed", [n for n in named if n.startswith(("conv_in.", "time_embedding.", "add_embedding."))
-                                or ".time_emb_proj." in n]))
+        # the resnets' time_emb_proj weights, then their biases, each set back to back (the batched projection reads
+        # them as one [sum Co][tdim] matrix / [sum Co] vector: zero-copy views of the full-UNet working copy)
+        units.append(("embed", [n for n in named if n.startswith(("conv_in.", "time_embedding.", "add_embedding."))]
+                      + [n for n in named if n.endswith(".time_emb_proj.weight")]
+                      + [n for n in named if n.endswith(".time_emb_proj.bias")]))
         return units
 
     def grad_unit_ranges(self):
@@ -1090,9 +1113,9 @@ class UNet2DConditionModel(nn.Module):
         self.full = FullGradState(self)
         return self.full
 
-    def refresh_full(self):
+    def refresh_full(self, cast=True):
         """After an optimizer step on self.full.master: bf16 module weights + kernel-layout caches."""
-        self.full.refresh()
+        self.full.refresh(cast)
         self.prepare()
 
     def disable_adapters(self):
@@ -1111,8 +1134,8 @@ class UNet2DConditionModel(nn.Module):
                 m.prepare()
         # the time-embedding projections of all resnets as ONE GEMM
         res = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
-        self._temb_w = torch.cat([m.time_emb_proj.weight.data for m in res], 0)
-        self._temb_b = torch.cat([m.time_emb_proj.bias.data for m in res], 0)
+        self._temb_w = _stacked([m.time_emb_proj.weight.data for m in res])
+        self._temb_b = _stacked([m.time_emb_proj.bias.data for m in res])
         off = 0
         for m in res:
             m._temb_off = off
@@ -1143,8 +1166,8 @@ class UNet2DConditionModel(nn.Module):
         if self.lora is not None:
             self.refresh_lora()
 
-    def refresh_lora(self):
-        self.lora.refresh()
+    def refresh_lora(self, cast=True):
+        self.lora.refresh(cast)
 
     # ---------------- fp8 forward (BASELINE config 5) ----------------
     def enable_fp8_forward(self, on=True):
@@ -1415,11 +1438,18 @@ class UNet2DConditionModel(nn.Module):
         e = rt.emb
         dt = K.cast_f32_bf16(rt.dtemb)
         res = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
-        tmp = torch.zeros((self._temb_n, e["se"].shape[1]), device=dt.device, dtype=torch.float32)
-        K.gemm_tn(dt, e["se"], tmp)
-        for m in res:
-            fg.g(m.time_emb_proj.weight).add_(tmp[m._temb_off:m._temb_off + m.cout])
-            fg.g(m.time_emb_proj.bias).add_(rt.dtemb[:, m._temb_off:m._temb_off + m.cout].sum(0))
+        gw = _stacked([fg.g(m.time_emb_proj.weight) for m in res])
+        gb = _stacked([fg.g(m.time_emb_proj.bias) for m in res])
+        if gw.data_ptr() == fg.g(res[0].time_emb_proj.weight).data_ptr() and \
+                gb.data_ptr() == fg.g(res[0].time_emb_proj.bias).data_ptr():  # adjacent grads: accumulate in place
+            K.gemm_tn(dt, e["se"], gw)
+            gb.add_(rt.dtemb.sum(0))
+        else:
+            tmp = torch.zeros((self._temb_n, e["se"].shape[1]), device=dt.device, dtype=torch.float32)
+            K.gemm_tn(dt, e["se"], tmp)
+            for m in res:
+                fg.g(m.time_emb_proj.weight).add_(tmp[m._temb_off:m._temb_off + m.cout])
+                fg.g(m.time_emb_proj.bias).add_(rt.dtemb[:, m._temb_off:m._temb_off + m.cout].sum(0))
 
         def silu_bwd(dy, x):
             xf = x.float()

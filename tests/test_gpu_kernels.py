@@ -574,12 +574,14 @@ def test_adamw8bit_vs_restatement(cuda, n):
     for step in range(1, 6):
         gr = np.zeros(npad, np.float32)
         gr[:n] = (g_.standard_normal(n) * np.exp(g_.standard_normal(n))).astype(np.float32) * 1e-2
-        K_.adamw8bit_step(pd, torch.tensor(gr[:n], device=cuda), st, lr, (b1, b2), eps, wd, step)
+        wb = torch.full((n,), float("nan"), device=cuda, dtype=torch.bfloat16) if step == 5 else None
+        K_.adamw8bit_step(pd, torch.tensor(gr[:n], device=cuda), st, lr, (b1, b2), eps, wd, step, out_bf16=wb)
         p, qm, qv, am, av = O.adamw8bit_step(p, gr, qm, qv, am, av, lr, b1, b2, eps, wd, step)
     torch.cuda.synchronize()
     assert np.array_equal(st.am.cpu().numpy(), am) and np.array_equal(st.av.cpu().numpy(), av)
     assert (st.qm.cpu().numpy() == qm[:n]).mean() > 0.9999 and (st.qv.cpu().numpy() == qv[:n]).mean() > 0.9999
     assert np.abs(pd.cpu().numpy() - p[:n]).max() <= 1e-6 * np.abs(p).max()
+    assert torch.equal(wb, pd.bfloat16())  # the fused bf16 working copy = RNE cast of the updated parameters
     # it is an Adam step: against fp32 AdamW the parameters move the same way (codes cost a few % of the update)
     m, v = st.dequant()
     assert torch.isfinite(m).all() and (v >= 0).all()

@@ -255,3 +255,38 @@ def test_transpose_im2col_sumpool_weight_t(cuda):
     wt = torch.randn(16, 3, 3, 8, device=cuda).bfloat16()
     assert torch.equal(K.conv_weight_t(wt, True), wt.flip(1, 2).permute(3, 1, 2, 0).contiguous())
     assert torch.equal(K.conv_weight_t(wt, False), wt.permute(3, 1, 2, 0).contiguous())
+
+
+@pytest.mark.parametrize("shape", [(640, 3, 3, 320), (1280, 3, 3, 2560), (4, 3, 3, 320), (320, 3, 3, 4), (100, 1, 1, 72),
+                                   (70, 3, 3, 12)])
+def test_conv_weight_t_shapes(cuda, shape):
+    """Tiled per-tap transpose of the conv weights (16-B row reads when Ci % 8 == 0, ragged tiles, Ci or Co < 64)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    wt = torch.randn(*shape, device=cuda).bfloat16()
+    assert torch.equal(K.conv_weight_t(wt, True), wt.flip(1, 2).permute(3, 1, 2, 0).contiguous())
+    assert torch.equal(K.conv_weight_t(wt, False), wt.permute(3, 1, 2, 0).contiguous())
+
+
+@pytest.mark.parametrize("rc", [(1280, 1280), (10240, 1280), (1280, 5120), (77, 2048), (130, 300), (64, 8)])
+def test_transpose_shapes(cuda, rc):
+    """Transposes of whole tensors and of column-sliced views (ld > C, unaligned column offset -> scalar reads)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    R, C = rc
+    x = torch.randn(R, C + 24, device=cuda).bfloat16()
+    assert torch.equal(K.transpose(x), x.t().contiguous())
+    assert torch.equal(K.transpose(x[:, 8:8 + C]), x[:, 8:8 + C].t().contiguous())
+    assert torch.equal(K.transpose(x[:, 3:3 + C]), x[:, 3:3 + C].t().contiguous())
+
+
+@pytest.mark.parametrize("n", [8, 1003, 4096 * 37 + 5, 1 << 22])
+def test_casts_vectorised_and_ragged(cuda, n):
+    from pairwise_sample_optimization_amd import kernels as K
+    x = torch.randn(n + 3, device=cuda) * 3
+    for off in (0, 1):  # 16-B aligned -> 8-wide path + tail; unaligned -> scalar path
+        xs = x[off:off + n]
+        assert torch.equal(K.cast_f32_bf16(xs), xs.bfloat16())
+        assert torch.equal(K.cast_f32_bf16(xs, scale=0.5), (xs * 0.5).bfloat16())
+        b = xs.bfloat16()
+        y = torch.empty(n + 4, device=cuda)
+        K.cast_bf16_f32(b, out=y[off:off + n])
+        assert torch.equal(y[off:off + n], b.float())
