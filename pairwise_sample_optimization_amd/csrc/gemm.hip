@@ -794,7 +794,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
   const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
-                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45)
+                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47)
                      ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
@@ -847,7 +847,8 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
                        (!g.bias || al8(g.bias)) && (!g.rowbias || (al8(g.rowbias) && g.rows_per_group == hw)) &&
                        fits30((long)g.M + 2L * (cv.W + 1), cv.C1) && fits30(g.N, g.ldb1) && al16(g.a1) && al16(g.b1);
     const long t320c = (long)(g.M / 256) * (g.N / 320);
-    if (conv8 && gv_raw != 43 && (gv_raw == 44 || (gv == 0 && t320c >= 256)))
+    const long min320c = (gv_raw == 46 || gv_raw == 47) ? 256 : 192;
+    if (conv8 && gv_raw != 43 && (gv_raw == 44 || (gv == 0 && t320c >= min320c)))
       return pso_gemm8p320_conv_run(g.M / (int)hw, cv.H, cv.W, cv.C1, g.a1, g.b1, g.N, g.alpha, g.bias, g.rowbias,
                                     g.ld_rowbias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   }
@@ -862,7 +863,15 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
                      (!g.a2 || (fits30(g.tail_m, g.lda2) && fits30(g.N, g.ldb2)));
   const bool ok8 = base8 && (g.N % 256) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 256) == 0);
   const long t256 = (long)((g.M + 255) / 256) * (g.N / 256);
-  if (ok8 && (gv == 30 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
+  // wide N (>= 2560) whose 256 x 256 tiles leave a partial round while the 256 x 320 ones make whole rounds (C3's
+  // 6144 x 10240 x 1280: 960 vs 768 tiles, 979 vs 1079 TF/s; 24576 x 5120 x 640: 802 vs 832) take the 320 form below;
+  // variant 46 keeps the round-2 rules
+  const bool ok320w = base8 && (g.N % 320) == 0 && g.lda1 == g.ldb1 && (!g.a2 || g.K2 <= 64) &&
+                      (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
+  const long t320w = (long)((g.M + 255) / 256) * (g.N / 320);
+  const bool wide320 = gv == 0 && gv_raw != 46 && ok320w && g.N >= 2560 && (t256 % 256) != 0 && t320w >= 256 &&
+                       (t320w % 256) == 0;
+  if (ok8 && !wide320 && (gv == 30 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);
@@ -881,8 +890,13 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const bool ok320 = base8 && (g.N % 320) == 0 && g.lda1 == g.ldb1 && (!g.a2 || g.K2 <= 64) &&
                      (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
   const long t320 = (long)((g.M + 255) / 256) * (g.N / 320);
+  // three quarters of a round already beats the 2-phase tiles (C4's 12288 x 1280 x 5120: 1072 vs 811 TF/s, x 1280:
+  // 875 vs 830; C3's 24576 x 640 x 2560: 1034 vs 725, x 640: 685 vs 612 -- 192 tiles each); half a round does not
+  // (8192 x 1280 x 1280: 574 vs 776).  Variant 46 / 47 keep the full-round rule.
+  const long min320 = (gv_raw == 46 || gv_raw == 47) ? 256 : 192;
   if (ok320 && gv_raw != 40 && gv_raw != 38 &&
-      (gv_raw == 39 || (gv == 0 && t320 >= 256 && g.N < 2560 && (gv_raw != 42 || Ktot < 2560))))
+      (gv_raw == 39 || wide320 ||
+       (gv == 0 && t320 >= min320 && g.N < 2560 && (gv_raw != 42 || Ktot < 2560))))
     return pso_gemm8p320_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
   const bool ok160 = base8 && (g.N % 160) == 0 && (!g.a2 || g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
@@ -925,6 +939,12 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // tiles).  tools/gemm_bench.py at 8 images: L2 ff.out 8192x1280x5120 797 -> 1097 TF/s, L2 proj 636 -> 816,
   // L0/L1/L2 3x3 convs 733/887/795 -> 921/994/1005.
   if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= 1024) return launch<256, 256, 2, 4, 2>(g, st);
+  // 128 x 160 tiles that leave a quarter of the 512 co-resident slots empty while 128 x 128 ones nearly fill them
+  // (C3's 6144-row L2 products, N = 1280: 384 vs 480 tiles; proj 678 -> 753 TF/s, ff.out 860 -> 971, GEGLU dX
+  // 940 -> 1023, 3x3 conv 802 -> 864): the 8-wave 128 x 128 kernel.  Variant 46 keeps the 128 x 160 choice.
+  if (gv_raw != 46 && !bn64_only && n160 && tiles(128, 160) < 512 && tiles(128, 128) <= 512 &&
+      tiles(128, 128) > tiles(128, 160))
+    return launch<128, 128, 2, 4, 2>(g, st);
   if (n160 && tiles(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
   if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= (g.conv.mode ? 128 : 256))
     return launch<256, 256, 2, 4, 2>(g, st);

@@ -154,7 +154,9 @@ def _stacked(ws):
     """torch.cat(ws, 0) of same-width row-major weights -- as a zero-copy view when they already lie back to back in
     memory (the full-UNet flat working copy keeps a block's q/k/v, and k/v, adjacent), else a new tensor."""
     w0 = ws[0]
-    adjacent = all(w.is_contiguous() and w.dtype == w0.dtype and w.shape[1:] == w0.shape[1:] for w in ws)
+    base = w0.untyped_storage().data_ptr()
+    adjacent = all(w.is_contiguous() and w.dtype == w0.dtype and w.shape[1:] == w0.shape[1:] and
+                   w.untyped_storage().data_ptr() == base for w in ws)  # one storage (not merely adjacent blocks)
     if adjacent:
         off = w0.data_ptr()
         for w in ws:
@@ -162,7 +164,7 @@ def _stacked(ws):
             off += w.numel() * w.element_size()
     if adjacent:
         rows = sum(w.shape[0] for w in ws)
-        return torch.as_strided(w0, (rows,) + tuple(w0.shape[1:]), w0.stride())
+        return torch.as_strided(w0, (rows,) + tuple(w0.shape[1:]), w0.stride(), w0.storage_offset())
     return torch.cat(ws, 0)
 
 
