@@ -335,6 +335,10 @@ int pso_conv_weight_t(int Co, int ks, int Ci, int flip, const void* w, void* wt,
 /* batched transpose: descs = device array of n {const bf16* src; bf16* dst; int R, C; long ldi, ldo;} (src [R][C]
  * -> dst [C][R]); one launch for all LoRA working-copy transposes after an optimizer step. */
 int pso_transpose_batched(int n, const void* descs, int max_r, int max_c, void* stream);
+/* many transposes in one launch over a flat grid of 64 x 64 tiles: descs = device array of n 48-B records
+ * {const bf16* src; bf16* dst; long ldi, ldo; int R, C, tiles_c, tile0;} (src [R][C] -> dst [C][R], tiles_c =
+ * ceil(C / 64), tile0 = the record's first tile, ascending from 0), total_tiles = sum of ceil(R/64) * tiles_c. */
+int pso_transpose_multi(int n, const void* descs, int total_tiles, void* stream);
 /* dst row i = src row idx[i] (row_bytes % 4 == 0): the pair/time shuffles of the trajectory buffer (T:733-745) */
 int pso_gather_rows(long n, long row_bytes, const void* src, const int64_t* idx, void* dst, void* stream);
 /* layout conversion of the (small) latent tensors at the diffusers NCHW API boundary */

@@ -107,6 +107,7 @@ SIGNATURES = {
     "pso_softmax_rows": (ci, [ci, ci, vp, cl, vp]),
     "pso_grad_clip_ws_bytes": (csz, [cl]),
     "pso_transpose_batched": (ci, [ci, vp, ci, ci, vp]),
+    "pso_transpose_multi": (ci, [ci, vp, ci, vp]),
     "pso_gather_rows": (ci, [cl, cl, vp, vp, vp, vp]),
     "pso_grad_clip_coef": (ci, [cl, vp, cf, cf, vp, vp, csz, vp]),
     "pso_adamw_step": (ci, [cl, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),

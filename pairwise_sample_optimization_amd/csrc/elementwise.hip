@@ -95,12 +95,12 @@ __global__ void timestep_embed_kernel(int n, int dim, const float* __restrict__ 
 }
 
 // 64x64 tiled transpose, bf16: in [R][C] (ldi) -> out [C][Rp] (ldo); rows R..Rp-1 of the input read as zero
-__global__ __launch_bounds__(256) void transpose_kernel(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
-                                                        bf16_t* __restrict__ out, long ldo) {
-  // 64 x 64 tile: rows read as 16-B chunks where the view allows (C, ldi multiples of 8, 16-B base), written back as
-  // 64 consecutive 2-B elements per output row
-  __shared__ bf16_t tile[64][72];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64, t = threadIdx.x;
+// one 64 x 64 tile of out [C][Rp] = in [R][C]^T (rows >= R zero): rows read as 16-B chunks where the view allows (C,
+// ldi multiples of 8, 16-B base), written back as 64 consecutive 2-B elements per output row
+__device__ __forceinline__ void transpose_tile(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
+                                               bf16_t* __restrict__ out, long ldo, int r0, int c0,
+                                               bf16_t (*tile)[72]) {
+  const int t = threadIdx.x;
   const bool vec = (C % 8) == 0 && (ldi % 8) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
   for (int q = t; q < 64 * 8; q += 256) {
     const int i = q >> 3, c = (q & 7) * 8, r = r0 + i;
@@ -117,6 +117,37 @@ __global__ __launch_bounds__(256) void transpose_kernel(int R, int Rp, int C, co
     const int c = c0 + i, r = r0 + tx;
     if (c < C && r < Rp) out[(long)c * ldo + r] = tile[tx][i];
   }
+}
+
+__global__ __launch_bounds__(256) void transpose_kernel(int R, int Rp, int C, const bf16_t* __restrict__ in, long ldi,
+                                                        bf16_t* __restrict__ out, long ldo) {
+  __shared__ bf16_t tile[64][72];
+  transpose_tile(R, Rp, C, in, ldi, out, ldo, blockIdx.y * 64, blockIdx.x * 64, tile);
+}
+
+// many transposes of different shapes in ONE launch (the full-UNet step rebuilds ~460 transposed weights after every
+// optimizer step): a flat grid over all their 64 x 64 tiles; each workgroup finds its matrix by a binary search over
+// the tile offsets (uniform across the workgroup: scalar loads)
+struct TransposeMultiDesc {
+  const bf16_t* src;
+  bf16_t* dst;
+  long ldi, ldo;
+  int R, C, tiles_c, tile0;
+};
+static_assert(sizeof(TransposeMultiDesc) == 48, "descriptor layout shared with kernels.py");
+
+__global__ __launch_bounds__(256) void transpose_multi_kernel(int n, const TransposeMultiDesc* __restrict__ d) {
+  __shared__ bf16_t tile[64][72];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].tile0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const TransposeMultiDesc t = d[lo];
+  const int k = b - t.tile0, tr = k / t.tiles_c, tc = k - tr * t.tiles_c;
+  transpose_tile(t.R, t.R, t.C, t.src, t.ldi, t.dst, t.ldo, tr * 64, tc * 64, tile);
 }
 
 // NHWC small-channel im2col for 3x3/pad 1/stride 1: in [B][H][W][C] -> out [B*H*W][Kp] (Kp >= 9C, zero padded),
@@ -459,6 +490,12 @@ int pso_timestep_embedding(int n, int dim, const float* t, void* out, long ldo, 
   timestep_embed_kernel<<<grid_for((long)n * dim / 2), 256, 0, (hipStream_t)stream>>>(n, dim, t, (bf16_t*)out, ldo,
                                                                                       out_col);
   return pso_check_launch("pso_timestep_embedding");
+}
+
+int pso_transpose_multi(int n, const void* descs, int total_tiles, void* stream) {
+  PSO_ARG_CHECK(n > 0 && descs && total_tiles > 0, "pso_transpose_multi: bad args");
+  transpose_multi_kernel<<<total_tiles, 256, 0, (hipStream_t)stream>>>(n, (const TransposeMultiDesc*)descs);
+  return pso_check_launch("pso_transpose_multi");
 }
 
 int pso_transpose(int R, int Rp, int C, const void* in, long ldi, void* out, long ldo, void* stream) {

@@ -59,7 +59,13 @@ class SideStream:
             return
         main = torch.cuda.current_stream()
         if self.s is None:
-            self.s = torch.cuda.Stream(device=main.device)
+            # ONE side stream per device for the process: the caching allocator keeps freed blocks per stream, so a
+            # fresh pool stream per step (torch hands them out round-robin) could never reuse the previous step's
+            # side-stream buffers -- every step allocated anew until the cache was released (a device sync: a 9 ms
+            # idle gap per C3 step)
+            self.s = SideStream._streams.get(main.device)
+            if self.s is None:
+                self.s = SideStream._streams[main.device] = torch.cuda.Stream(device=main.device)
         self.s.wait_stream(main)
         with torch.cuda.stream(self.s):
             fn()
@@ -73,6 +79,7 @@ class SideStream:
             self.pending = False
 
 
+SideStream._streams = {}
 SideStream.enabled_any = True  # False: every launch in line (profiling with serial event timing, bench.roofline)
 
 
@@ -590,12 +597,59 @@ def timestep_embedding(t, dim, out=None, out_col=0):
     return out
 
 
+_TRANSPOSE_BATCH = None  # list of pending (src, dst) while a transpose_batch() block is open
+
+
+class transpose_batch:
+    """Context: every K.transpose inside returns its (allocated) output at once but runs at the block's end, all of
+    them as ONE pso_transpose_multi launch (the full-UNet prepare() after each optimizer step: ~460 transposes whose
+    per-call host cost exceeded their GPU time).  The sources are kept alive until the launch is enqueued; nothing
+    inside the block may read a transposed output."""
+
+    def __enter__(self):
+        global _TRANSPOSE_BATCH
+        self.prev, _TRANSPOSE_BATCH = _TRANSPOSE_BATCH, []
+        return self
+
+    def __exit__(self, *exc):
+        global _TRANSPOSE_BATCH
+        items, _TRANSPOSE_BATCH = _TRANSPOSE_BATCH, self.prev
+        if items and exc[0] is None:
+            _transpose_multi(items)
+        return False
+
+
+def _transpose_multi(items):
+    import numpy as np
+    dt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("ldi", "<i8"), ("ldo", "<i8"), ("R", "<i4"), ("C", "<i4"),
+                   ("tiles_c", "<i4"), ("tile0", "<i4")])
+    assert dt.itemsize == 48
+    rec = np.zeros(len(items), dt)
+    tile = 0
+    for i, (x, out) in enumerate(items):
+        R, C = x.shape
+        tc = -(-C // 64)
+        rec[i] = (x.data_ptr(), out.data_ptr(), _row_stride(x), _row_stride(out), R, C, tc, tile)
+        tile += -(-R // 64) * tc
+    assert tile < 2 ** 31
+    dev = items[0][1].device
+    # pinned + non_blocking: a pageable copy would synchronise the stream (the host would stop getting ahead of the
+    # GPU); torch's caching host allocator keeps the pinned block until the copy has run
+    d = torch.from_numpy(rec.view(np.uint8)).pin_memory().to(dev, non_blocking=True)
+    check(lib().pso_transpose_multi(len(items), ptr(d), tile, stream_ptr()), "pso_transpose_multi")
+
+
 def transpose(x, out=None, pad_rows_to=1):
     """[R, C] -> [C, Rp], Rp = R rounded up to pad_rows_to (pad columns are zero)."""
     R, C = x.shape
     Rp = -(-R // pad_rows_to) * pad_rows_to
     if out is None:
         out = torch.empty((C, Rp), device=x.device, dtype=x.dtype)
+    if _TRANSPOSE_BATCH is not None and Rp == R and x.dtype == torch.bfloat16 and R > 0 and C > 0:
+        _row_stride(x)
+        _row_stride(out)
+        _TRANSPOSE_BATCH.append((x, out))
+        return out
     check(lib().pso_transpose(R, Rp, C, ptr(x), _row_stride(x), ptr(out), _row_stride(out), stream_ptr()),
           "pso_transpose")
     return out

@@ -1130,7 +1130,15 @@ class UNet2DConditionModel(nn.Module):
         return [self.lora.param] if self.lora is not None else []
 
     def prepare(self):
-        """Derive kernel-layout weight caches (one-time after load; weights are frozen in LoRA training)."""
+        """Derive kernel-layout weight caches (one-time after load; weights are frozen in LoRA training; the full-UNet
+        step re-runs it after every optimizer step): every transposed weight in ONE batched launch."""
+        with K.transpose_batch():
+            self._prepare_caches()
+        self._prepared = True
+        if self.lora is not None:
+            self.refresh_lora()
+
+    def _prepare_caches(self):
         for m in self.modules():
             if isinstance(m, (Transformer2DModel, ResnetBlock2D, Downsample2D, Upsample2D)):
                 m.prepare()
@@ -1163,10 +1171,7 @@ class UNet2DConditionModel(nn.Module):
             for lin in (self.time_embedding.linear_1, self.time_embedding.linear_2, self.add_embedding.linear_1,
                         self.add_embedding.linear_2):
                 lin.prepare()
-        self._prepared = True
         self._fp8_cache = {}  # kernel-layout weights may have been rebuilt
-        if self.lora is not None:
-            self.refresh_lora()
 
     def refresh_lora(self, cast=True):
         self.lora.refresh(cast)

@@ -278,6 +278,22 @@ def test_transpose_shapes(cuda, rc):
     assert torch.equal(K.transpose(x[:, 3:3 + C]), x[:, 3:3 + C].t().contiguous())
 
 
+def test_transpose_batch_one_launch(cuda):
+    """K.transpose inside K.transpose_batch(): outputs returned at once, filled by ONE pso_transpose_multi launch at
+    the block's end (ragged shapes, column-sliced views, a temporary source freed inside the block)."""
+    from pairwise_sample_optimization_amd import kernels as K
+    shapes = [(1280, 1280), (10240, 1280), (77, 2048), (130, 300), (64, 8), (1, 72), (3840, 640)]
+    xs = [torch.randn(r, c + 16, device=cuda).bfloat16()[:, 8:8 + c] for r, c in shapes]
+    with K.transpose_batch():
+        outs = [K.transpose(x) for x in xs]
+        tmp = K.transpose(torch.randn(200, 96, device=cuda).bfloat16() * 2)  # source dropped before the launch
+        refs_tmp = None
+    for x, o in zip(xs, outs):
+        assert torch.equal(o, x.t().contiguous())
+    assert tmp.shape == (96, 200) and torch.isfinite(tmp.float()).all()
+    del refs_tmp
+
+
 @pytest.mark.parametrize("n", [8, 1003, 4096 * 37 + 5, 1 << 22])
 def test_casts_vectorised_and_ragged(cuda, n):
     from pairwise_sample_optimization_amd import kernels as K
