@@ -251,10 +251,13 @@ def test_graph_epoch_equals_eager_epoch(cuda):
     # epoch 0 runs before any update: same kernels on the same inputs -> same loss.  Later epochs start from LoRA
     # weights that differ by the float-atomic rounding of the dW kernels, which beta = 50 and this test's large lr
     # (the loss falls 0.6 -> 0.08 in two updates) amplify; the graph replay must stay within that run-to-run spread
-    # (measured by the second eager run: 3x its spread, floor 2 % rel)
+    # (measured by the second eager run: 3x its spread, floor 5 % rel).  Two eager runs usually agree bit for bit, so
+    # the floor carries the bar: the replayed graph's atomic accumulation order is its own, and fresh boxes showed
+    # 2.2 % / 2.9 % at epochs 1 / 2 against eager (0.2228 vs 0.2279, 0.0779 vs 0.0802).  A replay on stale weights or
+    # inputs misses by the size of an epoch's change (0.60 -> 0.23 -> 0.08: > 60 %), far outside the floor.
     assert torch.allclose(le[0], lg[0], rtol=1e-5, atol=1e-6), (le, lg)
     spread = (le - le2).abs()
-    bar = torch.maximum(3 * spread, 2e-2 * le.abs()) + 1e-4
+    bar = torch.maximum(3 * spread, 5e-2 * le.abs()) + 1e-4
     assert ((le - lg).abs() <= bar).all(), (le, lg, le2)
     print(f"graph-vs-eager losses {lg.tolist()} vs {le.tolist()}, eager-vs-eager spread {spread.tolist()}")
     # the LoRA dW kernels accumulate with float atomics, so grads agree to rounding, not bitwise; AdamW turns a
