@@ -785,7 +785,6 @@ static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
-int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced group is used as given
 // raster group rows: C2-step sweep (tools/_var_ab.sh, same box) 2 / 3 / 4 / 5 / 6 / 8 / 16 -> 240.4 / 239.7 / 239.1 /
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
