@@ -152,11 +152,12 @@ void pso_attention_set_variant(int v);
  * dB = s dy^T u, reduction over tokens) without materialising transposes; split-K with f32 atomics. */
 int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                 long ldo, void* stream);
-/* pso_gemm_tn with a caller-owned fp32 workspace for the full-weight gradients (C3 / C4: both sides >= 128 wide):
- * when the 128 x 128 tiles alone leave CUs idle (I x J <= ~2 M, e.g. the 640^2 / 1280^2 weights), the reduction
- * rows are split over up to ws_bytes / (4 I J) slices whose partial products are STORED into ws and added into out
- * in slice order by a second kernel (deterministic; no f32 atomics).  pso_gemm_tn_ws_bytes(M, I, J) = the bytes
- * that enable the full split (0: no split applies); a smaller workspace gives fewer slices, 0 = pso_gemm_tn. */
+/* Deterministic pso_gemm_tn with a caller-owned fp32 workspace (the training path for every TN product): wherever the
+ * product splits its reduction rows (rank-16/32/64/96 side: the streaming rank kernel's row ranges; both sides >= 128:
+ * 128 x 128 tiles over slices, e.g. the 640^2 / 1280^2 weights; otherwise 64 x 64 tiles over slices), every split
+ * STORES its partial product into ws and a second kernel adds them into out in split order -- no f32 atomics, so two
+ * runs give the same bits.  pso_gemm_tn_ws_bytes(M, I, J) = the workspace that plan needs (0: no split, out += A^T B
+ * directly).  A smaller workspace falls back to pso_gemm_tn (atomic split). */
 size_t pso_gemm_tn_ws_bytes(int M, int I, int J);
 int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                    long ldo, void* ws, size_t ws_bytes, void* stream);
@@ -170,7 +171,7 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
  *   out_jc = 0 (dB = s dY^T u):  out[c][j]  += alpha * sum_m x[m][c] * u[m][(c / group_c) * R + j]   (out [C][R])
  *   out_jc = 1 (dA = v^T x):     out[j][c]  += alpha * sum_m x[m][c] * u[m][j]                       (out [R][C])
  * with x [M][C] (C % 128 == 0) the activation / output-gradient stream and u [M][*] the rank-R projection
- * (R = 32, 64 or 96), group_c = 0 or a multiple of 128 dividing C (the fused q/k/v adapters).  f32 atomics into
+ * (R = 16, 32, 64 or 96), group_c = 0 or a multiple of 128 dividing C (the fused q/k/v adapters).  f32 atomics into
  * out; probs is HOST memory, copied into the launch arguments (capturable in a hipGraph). */
 typedef struct {
   const void* x; long ldx;
@@ -180,6 +181,14 @@ typedef struct {
   float alpha;
 } PsoTnRankProblem;
 int pso_gemm_tn_rank_batch(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* stream);
+/* Deterministic form of pso_gemm_tn_rank_batch (the training path, TnRankQueue): no f32 atomics -- every workgroup
+ * STORES its 128 x R partial into the caller-owned device workspace ws and a second kernel adds the partials of each
+ * output block in row-range order, then out += alpha * sum.  Two runs, and a hipGraph replay, give the same bits (the
+ * reference's LoRA dW are cuBLAS GEMMs under autograd, T:857: a fixed reduction order).  Products whose outputs
+ * overlap go to separate launches.  pso_gemm_tn_rank_batch_ws_bytes = the workspace the call needs (0 on bad args). */
+size_t pso_gemm_tn_rank_batch_ws_bytes(int R, int out_jc, int count, const PsoTnRankProblem* probs);
+int pso_gemm_tn_rank_batch_ws(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* ws, size_t ws_bytes,
+                              void* stream);
 /* Grouped (block-diagonal) skinny product for the fused q/k/v LoRA adapters of the backward (v = dy sB per adapter):
  * out[m][g*N + n] = alpha * sum_k A[m][g*K + k] * W[n][g*K + k] for g < groups (bf16 out, N <= 128, N % 4 == 0). */
 int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
@@ -385,6 +394,16 @@ int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float*
                             uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v, float lr, float beta1, float beta2,
                             float eps, float weight_decay, int step, float grad_scale, const float* clip_coef,
                             void* stream);
+/* Per-tensor form (what bitsandbytes does with a list of parameter tensors, T:428-448): nblk blocks described by the
+ * device table desc [nblk][4] (int64: start element, length <= 2048, 32-bit state offset or -1, unused).  The blocks
+ * restart at every tensor, so one absmax never spans two tensors; a tensor under bitsandbytes' min_8bit_size (4096
+ * elements) keeps 32-bit state (no quantisation: m / v fp32 at exp_avg_32 / exp_avg_sq_32 + offset, same update),
+ * absmax_m / absmax_v hold one entry per table block.  Elements no block covers (alignment pads) are not touched.
+ * Non-finite gradient elements leave the parameter and its state unchanged.  param_bf16 may be NULL. */
+int pso_adamw8bit_step_blocks(long n, int nblk, const long* desc, float* param, void* param_bf16, const float* grad,
+                              uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v,
+                              float* exp_avg_32, float* exp_avg_sq_32, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream);
 int pso_zero_f32(long n, float* x, void* stream);
 int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
                    void* stream);

@@ -13,9 +13,13 @@ fixture of its optimizer); this restates the published algorithm (bitsandbytes `
                                 c1 = 1 - b1^t ; c2 = sqrt(1 - b2^t)
                                 p = p - lr * c2 / c1 * m / (sqrt(v) + c2 * eps)      then   p *= (1 - lr * wd)
                                 absmax' = max over the block of |m| (|v|);  q = nearest code of m / absmax' (v / ...)
-  * tensors below 4096 elements keep 32-bit state in bitsandbytes (`min_8bit_size`); every LoRA tensor of the SDXL
-    UNet is larger (r * 640 >= 10240) and a multiple of 2048, so blocks of the flat LoRA buffer never straddle two
-    tensors.
+  * bitsandbytes quantises every parameter tensor on its own: the 2048-blocks restart at each tensor (the last one
+    partial), and tensors below 4096 elements (`min_8bit_size`) keep 32-bit m / v with the same update
+    (kOptimizer32bit2State) -- `adamw8bit_step_tensors` restates that over a flat buffer and its tensor list;
+  * non-finite gradient elements: bitsandbytes skips their parameter update; here they leave p, m and v unchanged
+    (what bitsandbytes does to their state is not restated);
+  * the 2048-element block follows bitsandbytes' BLOCKSIZE_2STATE of the releases of the reference's time (the
+    reference pins no version; later releases may use other block sizes).
 """
 import numpy as np
 
@@ -81,3 +85,50 @@ def adamw8bit_step(p, g, qm, qv, am, av, lr, b1, b2, eps, wd, step):
     qm2 = quantize_nearest(sm.reshape(-1), cs)
     qv2 = quantize_nearest(sv.reshape(-1), cu)
     return pb.reshape(-1), qm2, qv2, am2, av2
+
+
+def _adam_update(p, m, v, g, lr, b1, b2, eps, wd, step):
+    """The element update of both bitsandbytes kernels (fp32), where g is finite; returns (p, m, v)."""
+    f = np.float32
+    ok = np.isfinite(g)
+    gz = np.where(ok, g, f(0))
+    m2 = f(b1) * m + f(1 - b1) * gz
+    v2 = f(b2) * v + f(1 - b2) * gz * gz
+    c1 = f(1 - b1 ** step)
+    c2 = f(np.sqrt(1 - b2 ** step))
+    step_size = f(-lr) * c2 / c1
+    p2 = (p + step_size * (m2 / (np.sqrt(v2) + c2 * f(eps)))) * f(1 - lr * wd)
+    return np.where(ok, p2, p).astype(f), np.where(ok, m2, m).astype(f), np.where(ok, v2, v).astype(f)
+
+
+MIN_8BIT_SIZE = 4096
+
+
+def adamw8bit_step_tensors(p, g, segments, state, lr, b1, b2, eps, wd, step):
+    """One AdamW8bit step over the parameter tensors segments = [(offset, numel)] of the flat fp32 buffers p / g, as
+    bitsandbytes runs it on a list of tensors (T:428-448).  state: dict offset -> per-tensor state, created on the
+    first call ({"m32", "v32"} under MIN_8BIT_SIZE, else {"qm", "qv", "am", "av"} with ceil(numel / BLOCK) blocks, the
+    last one partial).  Returns the new p (state updated in place)."""
+    cs, cu = create_dynamic_map(True), create_dynamic_map(False)
+    p = p.astype(np.float32).copy()
+    g = g.astype(np.float32)
+    for off, k in segments:
+        pt, gt = p[off:off + k], g[off:off + k]
+        if k < MIN_8BIT_SIZE:
+            st = state.setdefault(off, {"m32": np.zeros(k, np.float32), "v32": np.zeros(k, np.float32)})
+            p[off:off + k], st["m32"], st["v32"] = _adam_update(pt, st["m32"], st["v32"], gt, lr, b1, b2, eps, wd, step)
+            continue
+        nb = -(-k // BLOCK)
+        st = state.setdefault(off, {"qm": np.zeros(k, np.uint8), "qv": np.zeros(k, np.uint8),
+                                    "am": np.zeros(nb, np.float32), "av": np.zeros(nb, np.float32)})
+        for b in range(nb):
+            sl = slice(b * BLOCK, min(k, (b + 1) * BLOCK))
+            m = cs[st["qm"][sl]] * st["am"][b]
+            v = cu[st["qv"][sl]] * st["av"][b]
+            pb, m, v = _adam_update(pt[sl], m, v, gt[sl], lr, b1, b2, eps, wd, step)
+            p[off + sl.start:off + sl.stop] = pb
+            am, av = np.float32(np.abs(m).max()), np.float32(np.abs(v).max())
+            st["am"][b], st["av"][b] = am, av
+            st["qm"][sl] = quantize_nearest(m / am if am > 0 else np.zeros_like(m), cs)
+            st["qv"][sl] = quantize_nearest(v / av if av > 0 else np.zeros_like(v), cu)
+    return p

@@ -71,6 +71,8 @@ SIGNATURES = {
     "pso_gemm_tn_ws_bytes": (csz, [ci, ci, ci]),
     "pso_gemm_tn_ws": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp, csz, vp]),
     "pso_gemm_tn_rank_batch": (ci, [ci, ci, ci, vp, vp]),
+    "pso_gemm_tn_rank_batch_ws_bytes": (csz, [ci, ci, ci, vp]),
+    "pso_gemm_tn_rank_batch_ws": (ci, [ci, ci, ci, vp, vp, csz, vp]),
     "pso_gemm_skinny_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
     "pso_gemm_geglu": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, vp, cl, vp, cl, ci, vp]),
     "pso_gemm_geglu_bwd": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, vp, cl, vp]),
@@ -115,6 +117,8 @@ SIGNATURES = {
     "pso_adamw8bit_maps": (None, [vp, vp]),
     "pso_adamw8bit_step": (ci, [cl, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
     "pso_adamw8bit_step_bf16": (ci, [cl, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
+    "pso_adamw8bit_step_blocks": (ci, [cl, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf,
+                                       vp, vp]),
     "pso_zero_f32": (ci, [cl, vp, vp]),
     "pso_preference": (ci, [ci, ci, vp, vp, ci, vp, vp]),
     "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),

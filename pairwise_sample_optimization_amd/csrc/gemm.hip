@@ -785,6 +785,7 @@ static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
+int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced group is used as given
 // raster group rows: C2-step sweep (tools/_var_ab.sh, same box) 2 / 3 / 4 / 5 / 6 / 8 / 16 -> 240.4 / 239.7 / 239.1 /
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
@@ -975,7 +976,8 @@ __device__ __forceinline__ s16x4 tr_read64(const bf16_t* img, int r0, int col0, 
 
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int M, int I, int J, const bf16_t* __restrict__ A, long lda,
                                                          const bf16_t* __restrict__ B, long ldb, float alpha,
-                                                         float* __restrict__ out, long ldo) {
+                                                         float* __restrict__ out, long ldo,
+                                                         float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) bf16_t sA[2][64 * 64];
   __shared__ __attribute__((aligned(16))) bf16_t sB[2][64 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1062,7 +1064,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int M, int I, int J, co
       for (int r = 0; r < 4; ++r)
         if (j + r < J) {
           float* o = out + (long)i * ldo + j + r;
-          if (gridDim.y > 1) atomicAdd(o, acc[a][b][r] * alpha);
+          if (part) part[((long)blockIdx.y * I + i) * J + j + r] = acc[a][b][r] * alpha;  // ordered-reduction slice
+          else if (gridDim.y > 1) atomicAdd(o, acc[a][b][r] * alpha);
           else *o += acc[a][b][r] * alpha;
         }
     }
@@ -1217,39 +1220,97 @@ static int tn_ws_slices(int M, int I, int J) {
   return ks >= 2 ? ks : 0;
 }
 
+// Deterministic plan of a TN product with a caller-owned workspace (pso_gemm_tn_ws): every split of the reduction
+// rows stores its partial product and the partials are added in split order -- no f32 atomics anywhere.
+//   TNP_RANK:  one side a rank-16/32/64/96 projection -> the rank-r streaming kernel's workspace form
+//   TNP_128:   both sides >= 128 wide -> 128 x 128 tiles, ks slices (the small-weight split of tn_ws_slices, else the
+//              split the atomic form would take)
+//   TNP_64:    the rest -> 64 x 64 tiles, ks slices
+//   TNP_PLAIN: no split: out += directly (deterministic as it stands)
+enum { TNP_PLAIN = 0, TNP_RANK = 1, TNP_128 = 2, TNP_64 = 3 };
+struct TnPlan { int kind, ks, steps; size_t bytes; };
+static bool tn_rank_ok(int r) { return r == 16 || r == 32 || r == 64 || r == 96; }
+static TnPlan tn_plan(int M, int I, int J, long lda, long ldb) {
+  TnPlan p{TNP_PLAIN, 1, 0, 0};
+  if (M <= 0) return p;
+  if ((I % 128 == 0 && tn_rank_ok(J)) || (J % 128 == 0 && tn_rank_ok(I))) {
+    const bool x_is_a = I % 128 == 0 && tn_rank_ok(J);
+    PsoTnRankProblem q{};
+    q.x = (const void*)16; q.u = (const void*)16; q.out = (float*)16; q.ldx = 8; q.ldu = 8;
+    q.ldo = x_is_a ? J : I; q.M = M; q.C = x_is_a ? I : J; q.group_c = 0; q.alpha = 1.f;
+    p.kind = TNP_RANK;
+    p.bytes = pso_gemm_tn_rank_batch_ws_bytes(x_is_a ? J : I, x_is_a ? 0 : 1, 1, &q);
+    return p;
+  }
+  const int nkt = (M + 63) / 64;
+  if (I >= 128 && J >= 128 && (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30)) {
+    int ks = tn_ws_slices(M, I, J);
+    if (!ks) {  // the split the atomic form takes (pso_gemm_tn_grouped): ks <= M / 16384 where it yields >= 128 blocks
+      const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
+      ks = (512 + t128 - 1) / t128;
+      if (ks > M / 16384) ks = M / 16384;
+      if (ks < 1) ks = 1;
+      const int st0 = (nkt + ks - 1) / ks;
+      ks = (nkt + st0 - 1) / st0;
+      if (t128 * ks < 128) ks = 0;  // the 64 x 64 kernel's domain
+    }
+    if (ks >= 2) {
+      p.kind = TNP_128;
+      p.steps = (nkt + ks - 1) / ks;
+      p.ks = (nkt + p.steps - 1) / p.steps;
+      p.bytes = (size_t)p.ks * I * J * sizeof(float);
+      return p;
+    }
+    if (ks == 1) return p;
+  }
+  const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
+  int ks = (160 + tiles - 1) / tiles;
+  if (ks > nkt) ks = nkt;
+  if (ks >= 2) {
+    p.kind = TNP_64;
+    p.ks = ks;
+    p.bytes = (size_t)ks * I * J * sizeof(float);
+  }
+  return p;
+}
+
 extern "C" {
 
-size_t pso_gemm_tn_ws_bytes(int M, int I, int J) {
-  const int ks = tn_ws_slices(M, I, J);
-  return ks ? (size_t)ks * I * J * sizeof(float) : 0;
-}
+size_t pso_gemm_tn_ws_bytes(int M, int I, int J) { return tn_plan(M, I, J, I, J).bytes; }
 
 int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                    long ldo, void* ws, size_t ws_bytes, void* stream) {
-  int ks = tn_ws_slices(M, I, J);
-  if (ks && ws && (ldo % 4) == 0 && (((uintptr_t)out) & 15) == 0 && (((uintptr_t)ws) & 15) == 0 && (J % 4) == 0 &&
-      (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30) && g_tn_split == 0) {
-    PSO_ARG_CHECK(M >= 0 && A && B && out, "pso_gemm_tn_ws: bad args");
-    PSO_ARG_CHECK(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && (lda % 8) == 0 && (ldb % 8) == 0 &&
-                      (I % 8) == 0 && (J % 8) == 0,
-                  "pso_gemm_tn_ws: operands need 16-B aligned rows and I, J multiples of 8");
-    const long slice = (long)I * J * (long)sizeof(float);
-    if ((long)ws_bytes / slice < ks) ks = (int)((long)ws_bytes / slice);
-    if (ks >= 2) {
-      const int nkt = (M + 63) / 64;
-      const int steps = (nkt + ks - 1) / ks;
-      ks = (nkt + steps - 1) / steps;
+  PSO_ARG_CHECK(M >= 0 && I > 0 && J > 0 && A && B && out, "pso_gemm_tn_ws: bad args");
+  PSO_ARG_CHECK(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && (lda % 8) == 0 && (ldb % 8) == 0 &&
+                    (I % 8) == 0 && (J % 8) == 0,
+                "pso_gemm_tn_ws: operands need 16-B aligned rows and I, J multiples of 8");
+  if (M == 0) return PSO_OK;
+  const hipStream_t st = (hipStream_t)stream;
+  const TnPlan p = tn_plan(M, I, J, lda, ldb);
+  const bool ws_ok = ws && p.bytes && ws_bytes >= p.bytes && (((uintptr_t)ws) & 15) == 0 && g_tn_split == 0;
+  if (p.kind == TNP_RANK && ws_ok) {
+    const bool x_is_a = I % 128 == 0 && tn_rank_ok(J);
+    PsoTnRankProblem q{};
+    q.x = x_is_a ? A : B; q.ldx = x_is_a ? lda : ldb;
+    q.u = x_is_a ? B : A; q.ldu = x_is_a ? ldb : lda;
+    q.out = out; q.ldo = ldo; q.M = M; q.C = x_is_a ? I : J; q.group_c = 0; q.alpha = alpha;
+    return pso_gemm_tn_rank_batch_ws(x_is_a ? J : I, x_is_a ? 0 : 1, 1, &q, ws, ws_bytes, stream);
+  }
+  if ((p.kind == TNP_128 || p.kind == TNP_64) && ws_ok) {
+    const long n4 = (long)I * J / 4;
+    if (p.kind == TNP_128) {
       const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
       pso_note_kernel("gemm_tn128_kernel");
-      gemm_tn128_kernel<<<dim3(t128, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda,
-                                                                          (const bf16_t*)B, ldb, alpha, out, ldo,
-                                                                          steps, (float*)ws);
-      const long n4 = (long)I * J / 4;
-      tn_reduce_slices_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(I, J, ks,
-                                                                                            (const float*)ws, out,
-                                                                                            ldo);
-      return pso_check_launch("pso_gemm_tn_ws");
+      gemm_tn128_kernel<<<dim3(t128, p.ks), 256, 0, st>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, alpha,
+                                                          out, ldo, p.steps, (float*)ws);
+    } else {
+      const int tiles = ((I + 63) / 64) * ((J + 63) / 64);
+      pso_note_kernel("gemm_tn_kernel");
+      gemm_tn_kernel<<<dim3(tiles, p.ks), 256, 0, st>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, alpha,
+                                                        out, ldo, (float*)ws);
     }
+    tn_reduce_slices_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(I, J, p.ks, (const float*)ws, out, ldo);
+    return pso_check_launch("pso_gemm_tn_ws");
   }
   return pso_gemm_tn_grouped(M, I, J, A, lda, B, ldb, alpha, out, ldo, 0, stream);
 }
@@ -1427,7 +1488,7 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   if (M == 0) return PSO_OK;
   // One side a rank-r projection (LoRA): the streaming rank kernel.  group > 0 (block-diagonal fused q/k/v): the big
   // side's column c pairs with the small side's columns [(c / group) * r, +r) where r = small width / (big / group).
-  auto rk = [](int r) { return r == 32 || r == 64 || r == 96; };
+  auto rk = [](int r) { return r == 16 || r == 32 || r == 64 || r == 96; };
   if (g_tn_split == 0) {
     if (I % 128 == 0 && (group == 0 ? rk(J) : (group % 128 == 0 && I % group == 0 && rk(J / (I / group)))))
       return pso_gemm_tn_rank(M, I, A, lda, B, ldb, group ? J / (I / group) : J, group, alpha, out, ldo, 0,
@@ -1471,7 +1532,7 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   if (ks < 1) ks = 1;
   pso_note_kernel("gemm_tn_kernel");
   gemm_tn_kernel<<<dim3(tiles, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B,
-                                                                   ldb, alpha, out, ldo);
+                                                                   ldb, alpha, out, ldo, nullptr);
   return pso_check_launch("pso_gemm_tn");
 }
 

@@ -64,6 +64,8 @@ struct Gemm8Args {
   const bf16_t* rowbias; long ld_rowbias;
 };
 
+int pso_gemm_group_knob();  // gemm.hip: the raster-group benchmark knob (0 = automatic)
+
 namespace {
 
 constexpr int HT = 128 * 64;  // elements of one half-tile image [128 rows][64 k]
@@ -865,7 +867,19 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
   // the demangled name rocprofv3 reports (every template argument), so traces and live attribution agree
   pso_note_kernel("gemm8p_kernel<%d, %s, %s, %s, %d, %s>", EPI, STAG ? "true" : "false", SPRIO ? "true" : "false",
                   FP8 ? "true" : "false", BN, CONV ? "true" : "false");
-  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN, CONV><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(g);
+  // raster group aligned to the XCD chunks: each XCD walks nblk / 8 consecutive tile ids, so a group (group_m row
+  // bands x all column tiles) that straddles two chunks puts a row band's column tiles on two XCDs and its A rows
+  // are fetched into both L2s.  The largest group_m <= the requested one whose groups tile a chunk (C4's 12288 x
+  // 1280 x 5120, 192 tiles: 1.97 -> 1.66x algorithmic fetch; profiles/r03_pmc_raster.txt; whole-round shapes keep 4)
+  Gemm8Args ga = g;
+  const int nbn = g.N / BN;
+  if (pso_gemm_group_knob() == 0 && nblk >= 8 && nblk % 8 == 0) {  // (variant + 100 * rows forces a group)
+    const int chunk = nblk / 8;
+    int gm = g.group_m;
+    while (gm > 1 && chunk % (gm * nbn) != 0) --gm;
+    if (chunk % (gm * nbn) == 0) ga.group_m = gm;
+  }
+  gemm8p_kernel<EPI, STAG, SPRIO, FP8, BN, CONV><<<(BN == 160 && nblk > g_grid8) ? g_grid8 : nblk, 512, shm, st>>>(ga);
   return pso_check_launch(FP8 ? "pso_gemm_fp8" : "pso_gemm(8-phase)");
 }
 

@@ -1,8 +1,11 @@
 // Rank-r TN GEMM for gfx950: the LoRA weight gradients of the SDXL UNet.
 //
 //   D[c][j] = alpha * sum_m X[m][c] * U[m][j]      X: [M][C] (C >= 128, the activation / output gradient stream)
-//                                                  U: [M][R] (R = 16*NJT = 32 / 64 / 96, the rank-r projection)
-// accumulated (f32 atomics) into out[c][j] (dB = s dY^T u) or out[j][c] (dA = v^T x).  Replaces the reduction over the
+//                                                  U: [M][R] (R = 16*NJT = 16 / 32 / 64 / 96, the rank-r projection)
+// accumulated into out[c][j] (dB = s dY^T u) or out[j][c] (dA = v^T x): either with f32 atomics (pso_gemm_tn_rank_batch)
+// or -- the training path -- deterministically: every workgroup stores its 128 x R partial into a caller-owned
+// workspace and a second kernel adds the partials of each column block in row-range order (pso_gemm_tn_rank_batch_ws),
+// so two runs (and a hipGraph replay) give the same bits, as cuBLAS's fixed-order dW GEMMs do in the reference.  Replaces the reduction over the
 // B*S tokens inside peft's lora_A / lora_B weight gradients (`T:857` backward through `T:338-345`).
 //
 // The product is an HBM stream of X (2 FLOP per byte at R = 32).  Every 4-wave workgroup owns 128 columns of X and a
@@ -55,14 +58,15 @@ struct TnrProb {
   float* out; long ldo;
   int M, C, group_c, spb;
   float alpha; int blk0;
+  int rblk0;  // first block of this problem in the ordered-reduction launch (workspace form)
 };
 struct TnrBatch {
-  int count, nblk;
+  int count, nblk, nrblk;
   TnrProb p[TNR_MAXP];
 };
 
-template <int NJT, bool OUT_JC>
-__global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(TnrBatch bt) {
+template <int NJT, bool OUT_JC, bool WS>
+__global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(TnrBatch bt, float4* __restrict__ ws) {
   int pi = 0;
   for (int q = 1; q < bt.count; ++q)
     if ((int)blockIdx.x >= bt.p[q].blk0) pi = q;
@@ -189,6 +193,16 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(Tnr
         }
     }
   }
+  if constexpr (WS) {
+    // partial of this workgroup: 2*NJT float4 slots per thread, slot-major so every store is one coalesced 4 KB row
+    float4* dst = ws + (size_t)blockIdx.x * (2 * NJT * 256) + tid;
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int j = 0; j < NJT; ++j)
+        dst[(ci * NJT + j) * 256] = make_float4(acc[ci][j][0], acc[ci][j][1], acc[ci][j][2], acc[ci][j][3]);
+    return;
+  }
   if (n == 0) return;
   const int cw = c0 + wave * 32;
 #pragma unroll
@@ -202,15 +216,63 @@ __global__ __launch_bounds__(256, NJT == 6 ? 1 : 2) void gemm_tn_rank_kernel(Tnr
       }
 }
 
+// Ordered reduction of the workspace partials: thread t of column block cb of problem p owns float4 slot s of the
+// partial tile (the same (slot, thread) position every workgroup of that column block stored) and adds the partials
+// of the row ranges mb = 0, 1, ... in that order, then out += alpha * sum at the positions the atomic epilogue would
+// have used.  One thread per float4 slot: 2*NJT*256 threads per column block.
+template <int NJT, bool OUT_JC>
+__global__ __launch_bounds__(256) void tn_rank_reduce_kernel(TnrBatch bt, const float4* __restrict__ ws) {
+  constexpr int SLOTS = 2 * NJT;
+  const int gblk = blockIdx.x;  // one 256-thread block per (problem, column block, slot)
+  int pi = 0;
+  for (int q = 1; q < bt.count; ++q)
+    if (gblk >= bt.p[q].rblk0) pi = q;
+  const TnrProb& pr = bt.p[pi];
+  const int ncb = pr.C / 128;
+  const int l = gblk - pr.rblk0;
+  const int cb = l / SLOTS, slot = l - cb * SLOTS;
+  const int ci = slot / NJT, j = slot - ci * NJT;
+  const int nmb = (((pr.M + 63) / 64) + pr.spb - 1) / pr.spb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, cl = lane & 15;
+  const float4* src = ws + (size_t)(pr.blk0 + cb) * (SLOTS * 256) + slot * 256 + tid;
+  float4 s = src[0];
+  for (int mb = 1; mb < nmb; ++mb) {
+    const float4 v = src[(size_t)mb * ncb * (SLOTS * 256)];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float a[4] = {s.x, s.y, s.z, s.w};
+  const int cw = cb * 128 + wave * 32;
+  float* out = pr.out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float* o = OUT_JC ? out + (long)(j * 16 + 4 * g + r) * pr.ldo + cw + ci * 16 + cl
+                      : out + (long)(cw + ci * 16 + 4 * g + r) * pr.ldo + j * 16 + cl;
+    *o += a[r] * pr.alpha;
+  }
+}
+
 template <int NJT>
-int launch_tnr_batch(TnrBatch& bt, bool out_jc, hipStream_t st) {
+int launch_tnr_batch(TnrBatch& bt, bool out_jc, hipStream_t st, float4* ws = nullptr) {
   if (bt.count == 0) return PSO_OK;
+  if (ws) {
+    if (out_jc) {
+      pso_note_kernel("gemm_tn_rank_kernel<%d, true, true>", NJT);
+      gemm_tn_rank_kernel<NJT, true, true><<<bt.nblk, 256, 0, st>>>(bt, ws);
+      tn_rank_reduce_kernel<NJT, true><<<bt.nrblk, 256, 0, st>>>(bt, ws);
+    } else {
+      pso_note_kernel("gemm_tn_rank_kernel<%d, false, true>", NJT);
+      gemm_tn_rank_kernel<NJT, false, true><<<bt.nblk, 256, 0, st>>>(bt, ws);
+      tn_rank_reduce_kernel<NJT, false><<<bt.nrblk, 256, 0, st>>>(bt, ws);
+    }
+    return pso_check_launch("pso_gemm_tn_rank_batch_ws");
+  }
   if (out_jc) {
-    pso_note_kernel("gemm_tn_rank_kernel<%d, true>", NJT);
-    gemm_tn_rank_kernel<NJT, true><<<bt.nblk, 256, 0, st>>>(bt);
+    pso_note_kernel("gemm_tn_rank_kernel<%d, true, false>", NJT);
+    gemm_tn_rank_kernel<NJT, true, false><<<bt.nblk, 256, 0, st>>>(bt, nullptr);
   } else {
-    pso_note_kernel("gemm_tn_rank_kernel<%d, false>", NJT);
-    gemm_tn_rank_kernel<NJT, false><<<bt.nblk, 256, 0, st>>>(bt);
+    pso_note_kernel("gemm_tn_rank_kernel<%d, false, false>", NJT);
+    gemm_tn_rank_kernel<NJT, false, false><<<bt.nblk, 256, 0, st>>>(bt, nullptr);
   }
   return pso_check_launch("pso_gemm_tn(rank)");
 }
@@ -240,7 +302,7 @@ int launch_tnr(int M, int C, const bf16_t* X, long ldx, const bf16_t* U, long ld
   TnrBatch bt{};
   const int spb = tnr_spb(M, C, 16 * NJT, false);
   bt.count = 1;
-  bt.p[0] = TnrProb{X, ldx, U, ldu, out, ldo, M, C, group_c, spb, alpha, 0};
+  bt.p[0] = TnrProb{X, ldx, U, ldu, out, ldo, M, C, group_c, spb, alpha, 0, 0};
   bt.nblk = (C / 128) * ((((M + 63) / 64) + spb - 1) / spb);
   return launch_tnr_batch<NJT>(bt, out_jc, st);
 }
@@ -254,50 +316,120 @@ int pso_gemm_tn_rank(int M, int C, const void* X, long ldx, const void* U, long 
   auto x = (const bf16_t*)X;
   auto u = (const bf16_t*)U;
   switch (R) {
+    case 16: return launch_tnr<1>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
     case 32: return launch_tnr<2>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
     case 64: return launch_tnr<4>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
     case 96: return launch_tnr<6>(M, C, x, ldx, u, ldu, group_c, alpha, out, ldo, out_jc, st);
-    default: pso_set_error("pso_gemm_tn(rank): R must be 32, 64 or 96"); return PSO_ERR_ARG;
+    default: pso_set_error("pso_gemm_tn(rank): R must be 16, 32, 64 or 96"); return PSO_ERR_ARG;
   }
 }
 
-// Batched entry (pso_amd.h pso_gemm_tn_rank_batch): count products of one rank R and one orientation, in chunks of
-// TNR_MAXP per launch.
-extern "C" int pso_gemm_tn_rank_batch(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* stream) {
-  PSO_ARG_CHECK(R == 32 || R == 64 || R == 96, "pso_gemm_tn_rank_batch: R must be 32, 64 or 96 (R=%d)", R);
-  PSO_ARG_CHECK(count >= 0 && (count == 0 || probs), "pso_gemm_tn_rank_batch: bad problem list");
+// Batched entries (pso_amd.h pso_gemm_tn_rank_batch / _ws): count products of one rank R and one orientation, in
+// chunks of TNR_MAXP per launch.  A chunk never holds two products whose outputs overlap (the ordered reduction
+// writes out with plain read-modify-writes), and its workspace need is nblk * 128 * R floats.
+namespace {
+bool tnr_overlap(const PsoTnRankProblem& a, const PsoTnRankProblem& b, int R, int out_jc) {
+  auto span = [&](const PsoTnRankProblem& q, uintptr_t& lo, uintptr_t& hi) {
+    const long rows = out_jc ? R : q.C, cols = out_jc ? q.C : R;
+    lo = (uintptr_t)q.out;
+    hi = (uintptr_t)(q.out + (rows - 1) * q.ldo + cols);
+  };
+  uintptr_t a0, a1, b0, b1;
+  span(a, a0, a1);
+  span(b, b0, b1);
+  return a0 < b1 && b0 < a1;
+}
+
+// Fill the next chunk starting at probs[i]; returns the index after it.
+int tnr_chunk(TnrBatch& bt, int R, int out_jc, int count, const PsoTnRankProblem* probs, int i) {
+  bt = TnrBatch{};
+  int nblk = 0, nrblk = 0;
+  const int first = i;
+  for (; i < count && bt.count < TNR_MAXP; ++i) {
+    const PsoTnRankProblem& q = probs[i];
+    if (q.M == 0) continue;
+    bool clash = false;
+    for (int k = first; k < i && !clash; ++k)
+      clash = probs[k].M != 0 && tnr_overlap(probs[k], q, R, out_jc);
+    if (clash) break;
+    const int spb = tnr_spb(q.M, q.C, R, true);
+    const int nb = (q.C / 128) * ((((q.M + 63) / 64) + spb - 1) / spb);
+    bt.p[bt.count++] = TnrProb{(const bf16_t*)q.x, q.ldx, (const bf16_t*)q.u, q.ldu, q.out, q.ldo, q.M, q.C,
+                               q.group_c, spb, q.alpha, nblk, nrblk};
+    nblk += nb;
+    nrblk += (q.C / 128) * 2 * (R / 16);
+  }
+  bt.nblk = nblk;
+  bt.nrblk = nrblk;
+  return i;
+}
+
+int tnr_check(int R, int count, const PsoTnRankProblem* probs, const char* fn) {
+  PSO_ARG_CHECK(R == 16 || R == 32 || R == 64 || R == 96, "%s: R must be 16, 32, 64 or 96 (R=%d)", fn, R);
+  PSO_ARG_CHECK(count >= 0 && (count == 0 || probs), "%s: bad problem list", fn);
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   for (int i = 0; i < count; ++i) {
     const PsoTnRankProblem& q = probs[i];
     PSO_ARG_CHECK(q.x && q.u && q.out && q.M >= 0 && q.C > 0 && (q.C % 128) == 0,
-                  "pso_gemm_tn_rank_batch: problem %d: need C %% 128 == 0 and non-null operands", i);
+                  "%s: problem %d: need C %% 128 == 0 and non-null operands", fn, i);
     PSO_ARG_CHECK(al16(q.x) && al16(q.u) && (q.ldx % 8) == 0 && (q.ldu % 8) == 0,
-                  "pso_gemm_tn_rank_batch: problem %d: X / U need 16-B aligned rows", i);
+                  "%s: problem %d: X / U need 16-B aligned rows", fn, i);
     PSO_ARG_CHECK(q.group_c == 0 || ((q.group_c % 128) == 0 && (q.C % q.group_c) == 0),
-                  "pso_gemm_tn_rank_batch: problem %d: group_c must divide C in multiples of 128", i);
+                  "%s: problem %d: group_c must divide C in multiples of 128", fn, i);
   }
+  return PSO_OK;
+}
+
+int tnr_run(int R, int out_jc, TnrBatch& bt, hipStream_t st, float4* ws) {
+  switch (R) {
+    case 16: return launch_tnr_batch<1>(bt, out_jc != 0, st, ws);
+    case 32: return launch_tnr_batch<2>(bt, out_jc != 0, st, ws);
+    case 64: return launch_tnr_batch<4>(bt, out_jc != 0, st, ws);
+    default: return launch_tnr_batch<6>(bt, out_jc != 0, st, ws);
+  }
+}
+}  // namespace
+
+extern "C" int pso_gemm_tn_rank_batch(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* stream) {
+  int rc = tnr_check(R, count, probs, "pso_gemm_tn_rank_batch");
+  if (rc != PSO_OK) return rc;
   const hipStream_t st = (hipStream_t)stream;
   int i = 0;
   while (i < count) {
-    TnrBatch bt{};
-    int nblk = 0;
-    for (; i < count && bt.count < TNR_MAXP; ++i) {
-      const PsoTnRankProblem& q = probs[i];
-      if (q.M == 0) continue;
-      const int spb = tnr_spb(q.M, q.C, R, true);
-      const int nb = (q.C / 128) * ((((q.M + 63) / 64) + spb - 1) / spb);
-      bt.p[bt.count++] = TnrProb{(const bf16_t*)q.x, q.ldx, (const bf16_t*)q.u, q.ldu, q.out, q.ldo, q.M, q.C,
-                                 q.group_c, spb, q.alpha, nblk};
-      nblk += nb;
-    }
-    bt.nblk = nblk;
-    int rc;
-    switch (R) {
-      case 32: rc = launch_tnr_batch<2>(bt, out_jc != 0, st); break;
-      case 64: rc = launch_tnr_batch<4>(bt, out_jc != 0, st); break;
-      default: rc = launch_tnr_batch<6>(bt, out_jc != 0, st); break;
-    }
-    if (rc != PSO_OK) return rc;
+    TnrBatch bt;
+    i = tnr_chunk(bt, R, out_jc, count, probs, i);
+    if ((rc = tnr_run(R, out_jc, bt, st, nullptr)) != PSO_OK) return rc;
+  }
+  return PSO_OK;
+}
+
+extern "C" size_t pso_gemm_tn_rank_batch_ws_bytes(int R, int out_jc, int count, const PsoTnRankProblem* probs) {
+  if (tnr_check(R, count, probs, "pso_gemm_tn_rank_batch_ws_bytes") != PSO_OK) return 0;
+  size_t need = 0;
+  int i = 0;
+  while (i < count) {
+    TnrBatch bt;
+    i = tnr_chunk(bt, R, out_jc, count, probs, i);
+    const size_t b = (size_t)bt.nblk * 128 * R * sizeof(float);
+    if (b > need) need = b;
+  }
+  return need;
+}
+
+extern "C" int pso_gemm_tn_rank_batch_ws(int R, int out_jc, int count, const PsoTnRankProblem* probs, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  int rc = tnr_check(R, count, probs, "pso_gemm_tn_rank_batch_ws");
+  if (rc != PSO_OK) return rc;
+  PSO_ARG_CHECK(count == 0 || (ws && ((uintptr_t)ws & 15) == 0), "pso_gemm_tn_rank_batch_ws: need a 16-B aligned ws");
+  const hipStream_t st = (hipStream_t)stream;
+  int i = 0;
+  while (i < count) {  // chunks run in stream order and reuse the one workspace
+    TnrBatch bt;
+    i = tnr_chunk(bt, R, out_jc, count, probs, i);
+    PSO_ARG_CHECK((size_t)bt.nblk * 128 * R * sizeof(float) <= ws_bytes,
+                  "pso_gemm_tn_rank_batch_ws: workspace of %zu bytes is too small (need %zu)", ws_bytes,
+                  (size_t)bt.nblk * 128 * R * sizeof(float));
+    if ((rc = tnr_run(R, out_jc, bt, st, (float4*)ws)) != PSO_OK) return rc;
   }
   return PSO_OK;
 }

@@ -131,44 +131,94 @@ __device__ __forceinline__ int adam8_node(int i) {
   return (1 << (7 - h)) + ((i + 1) >> (h + 1));
 }
 
+// Block table (desc, optional): block b covers elements [desc[4b], desc[4b] + desc[4b+1]) of the flat buffers -- the
+// blocks restart at every tensor, as bitsandbytes quantises each parameter tensor on its own -- and desc[4b+2] >= 0
+// marks a block of a tensor under min_8bit_size (4096 elements) that keeps 32-bit state: m / v fp32 at
+// m32 / v32 + desc[4b+2] + (i - start).  desc == nullptr: uniform 2048-element blocks over [0, n), all 8-bit.
+// Non-finite gradient elements leave the parameter, m and v unchanged (bitsandbytes skips the parameter update for
+// them; its state update for such an element is not pinned here).
 __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
                                                         uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
                                                         float* __restrict__ am, float* __restrict__ av, float b1,
                                                         float omb1, float b2, float omb2, float eps_c2, float step_size,
                                                         float decay, float gscale, const float* __restrict__ clip,
-                                                        bf16_t* __restrict__ pw, Adam8Maps maps) {
+                                                        bf16_t* __restrict__ pw, const long* __restrict__ desc,
+                                                        float* __restrict__ m32, float* __restrict__ v32,
+                                                        Adam8Maps maps) {
 #pragma clang fp contract(off)
   __shared__ float cs[256], cu[256], ts[256], tu[256];
   __shared__ float red[2][4];
   const int t = threadIdx.x;
-  cs[t] = maps.s[t];
-  cu[t] = maps.u[t];
-  if (t < 255) {
-    ts[adam8_node(t)] = maps.s[t];
-    tu[adam8_node(t)] = maps.u[t];
-  }
   const long blk = blockIdx.x;
-  const long i0 = blk * ADAM8_BLOCK + (long)t * 8;
-  const bool full = i0 + 8 <= n;  // every thread of a block but the last block's tail: 32-B / 8-B vector accesses
+  long base = blk * ADAM8_BLOCK, end = min(n, base + ADAM8_BLOCK), soff = -1;
+  if (desc) {
+    base = desc[4 * blk];
+    end = base + desc[4 * blk + 1];
+    soff = desc[4 * blk + 2];
+  }
+  const bool st32 = soff >= 0;  // uniform over the workgroup
+  if (!st32) {
+    cs[t] = maps.s[t];
+    cu[t] = maps.u[t];
+    if (t < 255) {
+      ts[adam8_node(t)] = maps.s[t];
+      tu[adam8_node(t)] = maps.u[t];
+    }
+  }
+  const long i0 = base + (long)t * 8;
+  // 32-B / 8-B vector accesses wherever the thread's 8 elements are whole and aligned
+  const bool full = i0 + 8 <= end && (base & 7) == 0 && (!st32 || (soff & 3) == 0);
   const float s = gscale * (clip ? clip[1] : 1.0f);
-  const float am0 = am[blk], av0 = av[blk];
   float gv[8], pv[8];
-  uint32_t cm[2], cv[2];
   if (full) {
     const float4 g0 = *reinterpret_cast<const float4*>(g + i0), g1 = *reinterpret_cast<const float4*>(g + i0 + 4);
     const float4 p0 = *reinterpret_cast<const float4*>(p + i0), p1 = *reinterpret_cast<const float4*>(p + i0 + 4);
-    const uint2 qa = *reinterpret_cast<const uint2*>(qm + i0), qb = *reinterpret_cast<const uint2*>(qv + i0);
     gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
     pv[0] = p0.x; pv[1] = p0.y; pv[2] = p0.z; pv[3] = p0.w; pv[4] = p1.x; pv[5] = p1.y; pv[6] = p1.z; pv[7] = p1.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long i = i0 + e;
+      gv[e] = i < end ? g[i] : 0.f;
+      pv[e] = i < end ? p[i] : 0.f;
+    }
+  }
+  if (st32) {  // bitsandbytes 32-bit state (kOptimizer32bit2State ADAM): same arithmetic, no quantisation
+    float* ms = m32 + soff + (i0 - base);
+    float* vs = v32 + soff + (i0 - base);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (!(full || i0 + e < end)) continue;
+      const float gi = gv[e] * s;
+      if (!isfinite(gi)) continue;
+      float m = ms[e], v = vs[e];
+      m = (m * b1) + (omb1 * gi);
+      v = (v * b2) + ((omb2 * gi) * gi);
+      ms[e] = m;
+      vs[e] = v;
+      pv[e] = pv[e] + (step_size * (m / (sqrtf(v) + eps_c2)));
+      pv[e] = pv[e] * decay;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long i = i0 + e;
+      if (i >= end) continue;
+      p[i] = pv[e];
+      if (pw) pw[i] = f2bf(pv[e]);
+    }
+    return;
+  }
+  const float am0 = am[blk], av0 = av[blk];
+  uint32_t cm[2], cv[2];
+  if (full) {
+    const uint2 qa = *reinterpret_cast<const uint2*>(qm + i0), qb = *reinterpret_cast<const uint2*>(qv + i0);
     cm[0] = qa.x; cm[1] = qa.y; cv[0] = qb.x; cv[1] = qb.y;
   } else {
     cm[0] = cm[1] = cv[0] = cv[1] = 0u;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const long i = i0 + e;
-      gv[e] = i < n ? g[i] : 0.f;
-      pv[e] = i < n ? p[i] : 0.f;
-      if (i < n) {
+      if (i < end) {
         cm[e >> 2] |= (uint32_t)qm[i] << (8 * (e & 3));
         cv[e >> 2] |= (uint32_t)qv[i] << (8 * (e & 3));
       }
@@ -179,14 +229,16 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   float mx_m = 0.f, mx_v = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    if (full || i0 + e < n) {
+    if (full || i0 + e < end) {
       const float gi = gv[e] * s;
       m[e] = cs[(cm[e >> 2] >> (8 * (e & 3))) & 255u] * am0;
       v[e] = cu[(cv[e >> 2] >> (8 * (e & 3))) & 255u] * av0;
-      m[e] = (m[e] * b1) + (omb1 * gi);
-      v[e] = (v[e] * b2) + ((omb2 * gi) * gi);
-      pv[e] = pv[e] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
-      pv[e] = pv[e] * decay;
+      if (isfinite(gi)) {
+        m[e] = (m[e] * b1) + (omb1 * gi);
+        v[e] = (v[e] * b2) + ((omb2 * gi) * gi);
+        pv[e] = pv[e] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
+        pv[e] = pv[e] * decay;
+      }
       mx_m = fmaxf(mx_m, fabsf(m[e]));
       mx_v = fmaxf(mx_v, fabsf(v[e]));
     } else {
@@ -229,7 +281,7 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const long i = i0 + e;
-      if (i >= n) continue;
+      if (i >= end) continue;
       p[i] = pv[e];
       if (pw) pw[i] = f2bf(pv[e]);
       qm[i] = (uint8_t)im[e];
@@ -333,13 +385,10 @@ void pso_adamw8bit_maps(float* signed_map, float* unsigned_map) {
   adam8_dynamic_map(false, unsigned_map);
 }
 
-int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
-                       float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
-                       float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
-  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0,
-                "pso_adamw8bit_step_bf16: bad args");
-  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
-                "pso_adamw8bit_step_bf16: param / grad / param_bf16 need 16-B, the code arrays 8-B alignment");
+static int adam8_launch(long n, int nblk, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q,
+                        uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v, const long* desc, float* m32,
+                        float* v32, float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+                        float grad_scale, const float* clip_coef, void* stream) {
   static Adam8Maps maps = [] {
     Adam8Maps m;
     adam8_dynamic_map(true, m.s);
@@ -351,12 +400,40 @@ int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float*
   const float c2 = (float)std::sqrt(1.0 - std::pow(b2, step));
   const float step_size = (-lr) * c2 / c1;
   const float decay = (float)(1.0 - (double)lr * weight_decay);
-  const int nb = (int)pso_adamw8bit_blocks(n);
-  adamw8bit_kernel<<<nb, 256, 0, (hipStream_t)stream>>>(n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v,
-                                                         beta1, (float)(1.0 - b1), beta2, (float)(1.0 - b2),
-                                                         c2 * eps, step_size, decay, grad_scale, clip_coef,
-                                                         (bf16_t*)param_bf16, maps);
-  return pso_check_launch("pso_adamw8bit_step_bf16");
+  if (nblk <= 0) return PSO_OK;
+  adamw8bit_kernel<<<nblk, 256, 0, (hipStream_t)stream>>>(n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v,
+                                                           beta1, (float)(1.0 - b1), beta2, (float)(1.0 - b2),
+                                                           c2 * eps, step_size, decay, grad_scale, clip_coef,
+                                                           (bf16_t*)param_bf16, desc, m32, v32, maps);
+  return pso_check_launch("pso_adamw8bit_step");
+}
+
+int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,
+                       float* absmax_m, float* absmax_v, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
+  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0,
+                "pso_adamw8bit_step_bf16: bad args");
+  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
+                "pso_adamw8bit_step_bf16: param / grad / param_bf16 need 16-B, the code arrays 8-B alignment");
+  return adam8_launch(n, (int)pso_adamw8bit_blocks(n), param, param_bf16, grad, exp_avg_q, exp_avg_sq_q, absmax_m,
+                      absmax_v, nullptr, nullptr, nullptr, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
+                      clip_coef, stream);
+}
+
+int pso_adamw8bit_step_blocks(long n, int nblk, const long* desc, float* param, void* param_bf16, const float* grad,
+                              uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v,
+                              float* exp_avg_32, float* exp_avg_sq_32, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
+  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0 &&
+                    nblk >= 0 && (nblk == 0 || desc),
+                "pso_adamw8bit_step_blocks: bad args");
+  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16 | (uintptr_t)exp_avg_32 |
+                  (uintptr_t)exp_avg_sq_32) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
+                "pso_adamw8bit_step_blocks: param / grad / param_bf16 / 32-bit state need 16-B, the code arrays 8-B "
+                "alignment");
+  return adam8_launch(n, nblk, param, param_bf16, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, desc,
+                      exp_avg_32, exp_avg_sq_32, lr, beta1, beta2, eps, weight_decay, step, grad_scale, clip_coef,
+                      stream);
 }
 
 int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,

@@ -249,7 +249,7 @@ def gemm_fp8(a, w, *, a2=None, w2=None, tail_rows=0, tail_group_n=0, alpha=1.0, 
     return out
 
 
-TN_RANKS = (32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
+TN_RANKS = (16, 32, 64, 96)  # rank widths of the streaming TN kernel (grouped form needs one of them)
 
 
 def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
@@ -274,12 +274,15 @@ def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
 
 
 class TnRankQueue:
-    """Deferred LoRA weight-gradient products (gemm_tn calls whose one side is a rank-32/64/96 projection).  The
+    """Deferred LoRA weight-gradient products (gemm_tn calls whose one side is a rank-16/32/64/96 projection).  The
     backward records them as it goes (add) and issues them per gradient unit (flush) as ONE pso_gemm_tn_rank_batch
     launch per (rank, orientation): the ~700 rank-r products of a C2 step become a few dozen launches, each with
     enough workgroups to fill the chip, and fewer f32 atomics per byte streamed.  The queue holds a reference to
     every operand until its launch, so the caching allocator cannot recycle them early.  Products the rank kernel
     does not take run at once through gemm_tn (same arithmetic either way)."""
+
+    # PSO_TN_DETERMINISTIC=0 selects the f32-atomic epilogue (A/B knob); the default is the ordered workspace form
+    deterministic = os.environ.get("PSO_TN_DETERMINISTIC", "1") != "0"
 
     def __init__(self):
         self.pending = {}  # (R, out_jc) -> [(problem, operands, flop, bytes)]
@@ -306,7 +309,14 @@ class TnRankQueue:
         for (R, ojc), items in self.pending.items():
             arr = (_lib.PsoTnRankProblem * len(items))(*[it[0] for it in items])
             e0 = _prof_begin()
-            check(lib().pso_gemm_tn_rank_batch(R, ojc, len(items), arr, stream_ptr()), "pso_gemm_tn_rank_batch")
+            if TnRankQueue.deterministic:
+                # ordered reduction through a workspace (no f32 atomics): bit-identical runs and hipGraph replays
+                wsb = lib().pso_gemm_tn_rank_batch_ws_bytes(R, ojc, len(items), arr)
+                ws = torch.empty(max(int(wsb), 16), device=items[0][1][2].device, dtype=torch.uint8)
+                check(lib().pso_gemm_tn_rank_batch_ws(R, ojc, len(items), arr, ptr(ws), ws.numel(), stream_ptr()),
+                      "pso_gemm_tn_rank_batch_ws")
+            else:
+                check(lib().pso_gemm_tn_rank_batch(R, ojc, len(items), arr, stream_ptr()), "pso_gemm_tn_rank_batch")
             _prof_end(e0, sum(it[2] for it in items), sum(it[3] for it in items), ("gemm_tn_batch", R, ojc, len(items)))
         self.pending = {}
 
@@ -801,26 +811,77 @@ def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, s
 
 
 class Adam8State:
-    """State of the blockwise 8-bit AdamW (bitsandbytes AdamW8bit) for a flat fp32 parameter of n elements: uint8
-    codes of m and v, one fp32 absmax per 2048-element block of each; zero-initialised like bitsandbytes."""
+    """State of the blockwise 8-bit AdamW (bitsandbytes AdamW8bit) for a flat fp32 parameter buffer of n elements:
+    uint8 codes of m and v, one fp32 absmax per block of each; zero-initialised like bitsandbytes.
 
-    def __init__(self, n, device):
-        nb = lib().pso_adamw8bit_blocks(n)
+    segments = [(offset, numel)] of the parameter TENSORS inside the flat buffer (what bitsandbytes is handed at
+    T:428-448): blocks of 2048 restart at every tensor, and a tensor under MIN_8BIT_SIZE = 4096 elements (bitsandbytes'
+    min_8bit_size) keeps 32-bit m / v.  None: the whole buffer is one tensor (uniform blocks)."""
+
+    BLOCK = 2048
+    MIN_8BIT_SIZE = 4096
+
+    def __init__(self, n, device, segments=None):
+        self.n = n
         self.qm = torch.zeros(n, dtype=torch.uint8, device=device)
         self.qv = torch.zeros(n, dtype=torch.uint8, device=device)
-        self.am = torch.zeros(nb, dtype=torch.float32, device=device)
-        self.av = torch.zeros(nb, dtype=torch.float32, device=device)
+        self.desc = None
+        self.m32 = self.v32 = None
+        if segments is None:
+            nb = lib().pso_adamw8bit_blocks(n)
+            self.block_start = None
+        else:
+            rows, n32 = [], 0
+            for off, k in sorted(segments):
+                assert 0 <= off and off + k <= n, (off, k, n)
+                if k < self.MIN_8BIT_SIZE:  # 32-bit state, 8-aligned slot in the fp32 arrays
+                    for b0 in range(0, k, self.BLOCK):
+                        rows.append((off + b0, min(self.BLOCK, k - b0), n32 + b0, 0))
+                    n32 += -(-k // 8) * 8
+                else:
+                    for b0 in range(0, k, self.BLOCK):
+                        rows.append((off + b0, min(self.BLOCK, k - b0), -1, 0))
+            for (o1, l1, _, _), (o2, _, _, _) in zip(rows, rows[1:]):
+                assert o1 + l1 <= o2, "parameter segments overlap"
+            nb = len(rows)
+            self.desc = torch.tensor(rows, dtype=torch.int64).to(device)
+            self.block_start = torch.tensor([r[0] for r in rows], dtype=torch.int64)
+            self.rows = rows
+            self.m32 = torch.zeros(max(n32, 8), dtype=torch.float32, device=device)
+            self.v32 = torch.zeros(max(n32, 8), dtype=torch.float32, device=device)
+        self.nblk = int(nb)
+        self.am = torch.zeros(max(self.nblk, 1), dtype=torch.float32, device=device)
+        self.av = torch.zeros(max(self.nblk, 1), dtype=torch.float32, device=device)
 
     def dequant(self):
-        """(m, v) as fp32 (tests / checkpoints)."""
+        """(m, v) as fp32 over the flat buffer (tests / checkpoints; elements outside every tensor read 0)."""
         s = (ctypes.c_float * 256)()
         u = (ctypes.c_float * 256)()
         lib().pso_adamw8bit_maps(s, u)
-        cs = torch.tensor(list(s), device=self.qm.device)
-        cu = torch.tensor(list(u), device=self.qm.device)
+        dev = self.qm.device
+        cs = torch.tensor(list(s), device=dev)
+        cu = torch.tensor(list(u), device=dev)
         n = self.qm.numel()
-        blk = torch.arange(n, device=self.qm.device) // 2048
-        return cs[self.qm.long()] * self.am[blk], cu[self.qv.long()] * self.av[blk]
+        if self.desc is None:
+            blk = torch.arange(n, device=dev) // self.BLOCK
+            return cs[self.qm.long()] * self.am[blk], cu[self.qv.long()] * self.av[blk]
+        m = torch.zeros(n, device=dev)
+        v = torch.zeros(n, device=dev)
+        for b, (o, k, so, _) in enumerate(self.rows):
+            if so >= 0:
+                m[o:o + k] = self.m32[so:so + k]
+                v[o:o + k] = self.v32[so:so + k]
+            else:
+                m[o:o + k] = cs[self.qm[o:o + k].long()] * self.am[b]
+                v[o:o + k] = cu[self.qv[o:o + k].long()] * self.av[b]
+        return m, v
+
+    def tensors(self):
+        """The state tensors a checkpoint holds (name -> tensor)."""
+        out = {"exp_avg_q": self.qm, "exp_avg_sq_q": self.qv, "absmax_m": self.am, "absmax_v": self.av}
+        if self.desc is not None:
+            out.update(exp_avg_32=self.m32, exp_avg_sq_32=self.v32, block_table=self.desc)
+        return out
 
 
 def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None, out_bf16=None):
@@ -829,6 +890,14 @@ def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_
     require_cuda(param, grad)
     if out_bf16 is not None:
         assert out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == param.numel() and out_bf16.is_contiguous()
+    if state.desc is not None:
+        check(lib().pso_adamw8bit_step_blocks(param.numel(), state.nblk, ptr(state.desc), ptr(param), ptr(out_bf16),
+                                              ptr(grad), ptr(state.qm), ptr(state.qv), ptr(state.am), ptr(state.av),
+                                              ptr(state.m32), ptr(state.v32), float(lr), float(betas[0]),
+                                              float(betas[1]), float(eps), float(weight_decay), int(step),
+                                              float(grad_scale), ptr(clip), stream_ptr()),
+              "pso_adamw8bit_step_blocks")
+        return
     check(lib().pso_adamw8bit_step_bf16(param.numel(), ptr(param), ptr(out_bf16), ptr(grad), ptr(state.qm),
                                         ptr(state.qv), ptr(state.am), ptr(state.av), float(lr), float(betas[0]),
                                         float(betas[1]), float(eps), float(weight_decay), int(step), float(grad_scale),

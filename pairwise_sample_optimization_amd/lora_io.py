@@ -68,7 +68,7 @@ def save_state(trainer, output_dir):
     save_lora_weights(output_dir, peft_to_diffusers(get_peft_model_state_dict(unet)))
     a8 = getattr(trainer, "adam8", None)
     if a8 is not None:  # 8-bit AdamW state as it stands (codes + block absmax): a resume continues bit for bit
-        opt = {"exp_avg_q": a8.qm.cpu(), "exp_avg_sq_q": a8.qv.cpu(), "absmax_m": a8.am.cpu(), "absmax_v": a8.av.cpu()}
+        opt = {k: v.cpu() for k, v in a8.tensors().items()}
     else:
         opt = {"exp_avg": trainer.exp_avg.cpu(), "exp_avg_sq": trainer.exp_avg_sq.cpu()}
     save_file(opt, os.path.join(output_dir, OPT_NAME),
@@ -85,8 +85,13 @@ def load_state(trainer, input_dir):
     if a8 is not None:
         if "exp_avg_q" not in opt:
             raise KeyError("checkpoint holds fp32 AdamW state; this trainer runs the 8-bit AdamW (use_8bit_adam)")
-        for t, k in ((a8.qm, "exp_avg_q"), (a8.qv, "exp_avg_sq_q"), (a8.am, "absmax_m"), (a8.av, "absmax_v")):
-            t.copy_(opt[k])
+        mine = a8.tensors()
+        if ("block_table" in mine) != ("block_table" in opt) or (
+                "block_table" in opt and not torch.equal(opt["block_table"], mine["block_table"].cpu())):
+            raise KeyError("checkpoint's 8-bit AdamW block layout differs from this trainer's parameter tensors")
+        for k, t in mine.items():
+            if k != "block_table":
+                t.copy_(opt[k])
     else:
         if "exp_avg" not in opt:
             raise KeyError("checkpoint holds 8-bit AdamW state; this trainer runs fp32 AdamW")

@@ -212,6 +212,22 @@ def trainable(unet):
     return st.master, st.grad, st.refresh
 
 
+def trainable_segments(unet):
+    """[(offset, numel)] of the parameter tensors inside the flat trained buffer -- what the reference hands its
+    optimizer (T:428-448: the peft lora_A / lora_B weights, or every UNet parameter in full-UNet mode); the 8-bit
+    AdamW quantises each of them on its own (K.Adam8State)."""
+    if getattr(unet, "full", None) is not None:
+        fg = unet.full
+        return [(fg.offsets[nm][0], p.numel()) for nm, p in zip(fg.names, fg.params)]
+    st = unet.lora
+    base = st.master.data_ptr()
+    segs = []
+    for name in st.adapter_names():
+        for t in st.adapter_views(st.master, name):
+            segs.append(((t.data_ptr() - base) // st.master.element_size(), t.numel()))
+    return segs
+
+
 def _work_copy(unet, master):
     """The flat bf16 working copy that refresh() casts the master into (the optimizer can write it directly)."""
     st = unet.full if getattr(unet, "full", None) is not None else unet.lora
@@ -252,7 +268,8 @@ class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
                  train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None,
-                 latent_dtype=torch.float32, allreduce_dtype=None, use_8bit_adam=False):
+                 latent_dtype=torch.float32, allreduce_dtype=None, use_8bit_adam=False, overlap_sync=None,
+                 bucket_mb=32.0):
         self.unet = unet
         if mode not in ("turbo", "dmd"):
             raise ValueError(f"mode must be 'turbo' or 'dmd', got {mode!r}")
@@ -273,8 +290,10 @@ class PSOTrainer:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         master, _, _ = trainable(unet)
         # optimizer state: fp32 AdamW moments, or -- train.use_8bit_adam, the reference default (T:427-435) -- the
-        # blockwise 8-bit AdamW of bitsandbytes (uint8 codes + per-2048-block absmax, K.Adam8State)
-        self.adam8 = K.Adam8State(master.numel(), master.device) if use_8bit_adam else None
+        # blockwise 8-bit AdamW of bitsandbytes (uint8 codes + per-2048-block absmax, blocks restarting at every
+        # parameter tensor, 32-bit state under 4096 elements: K.Adam8State)
+        self.adam8 = K.Adam8State(master.numel(), master.device, segments=trainable_segments(unet)) \
+            if use_8bit_adam else None
         self.exp_avg = None if use_8bit_adam else torch.zeros_like(master)
         self.exp_avg_sq = None if use_8bit_adam else torch.zeros_like(master)
         self.opt_step = 0
@@ -286,11 +305,14 @@ class PSOTrainer:
         if getattr(unet, "full", None) is not None and ref_unet is None:
             raise ValueError("full-UNet training needs ref_unet (a frozen copy of the initial weights)")
         self.loss_hist = []
-        # overlapped bucketed all-reduce on multi-GPU runs (GradBuckets); off inside hipGraph capture
-        self.overlap_sync = self.world > 1
+        # overlapped bucketed all-reduce on multi-GPU runs (GradBuckets); off inside hipGraph capture.  overlap_sync
+        # forces it on (or off) whatever the world size: a world-1 RCCL group still runs every collective (tests)
+        self.overlap_sync = (self.world > 1) if overlap_sync is None else bool(overlap_sync)
+        if self.overlap_sync and not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("overlap_sync needs an initialised process group")
         self.allreduce_dtype = allreduce_dtype
         # allreduce_dtype=torch.bfloat16: bf16 on the wire, fp32 accumulation and optimizer (GradBuckets)
-        self.buckets = GradBuckets(unet, trainable(unet)[1], process_group=process_group,
+        self.buckets = GradBuckets(unet, trainable(unet)[1], bucket_mb=bucket_mb, process_group=process_group,
                                    wire_dtype=allreduce_dtype) if self.overlap_sync else None
         self.sync_armed = False
         self.max_pass_images = max_pass_images  # images per batched UNet pass (HBM budget: ~5 GB saved each @1024^2)

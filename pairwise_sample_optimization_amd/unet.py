@@ -622,12 +622,14 @@ class BasicTransformerBlock(nn.Module):
             v_q2 = K.gemm(dq2, L.sBt_q2)
             dn2 = K.gemm(dq2, a2m.to_q.wt, a2=v_q2, w2=L.At_q2)
             n2s, uq2, enc_, u_kv2 = sv["n2"], sv["u_q2"], rt.enc, sv["u_kv2"]
+            # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v] on the compute stream -- the deferred
+            # weight-gradient queue (rt.dw) is flushed there, so its operands must not come from the side stream
+            v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
 
             def dw_attn2():
                 rt.dw(v_q2, n2s, g("attn2.A_q"))
                 rt.dw(dq2, uq2, g("attn2.B_q"), st.scale)
-                # k/v adapters of the text tokens: v_kv = [dk sB_k | dv sB_v]; dA_kv += v_kv^T enc; dB_kv += s dkv^T u
-                v_kv = K.gemm_grouped_skinny(dkv2, L.sBt_kv2, 2)
+                # dA_kv += v_kv^T enc; dB_kv += s dkv^T u
                 rt.dw(v_kv, enc_, g("attn2.A_kv"))
                 gB = g("attn2.B_kv")
                 if r in K.TN_RANKS:
@@ -635,7 +637,7 @@ class BasicTransformerBlock(nn.Module):
                 else:
                     rt.dw(dkv2[:, :C], u_kv2[:, :r], gB[:C], st.scale)
                     rt.dw(dkv2[:, C:], u_kv2[:, r:], gB[C:], st.scale)
-            rt.side.launch(dw_attn2, v_q2, n2s, dq2, uq2, dkv2, enc_, u_kv2)
+            rt.side.launch(dw_attn2, v_q2, n2s, dq2, uq2, dkv2, enc_, u_kv2, v_kv)
         else:
             dn2 = K.gemm(dq2, a2m.to_q.wt)
         if fg is not None:

@@ -1,0 +1,79 @@
+"""Full-UNet (C3 / C4) policy vs frozen reference: with IDENTICAL weights the two forwards must return identical bits.
+
+The window loss of the full-UNet step (D:777-864, loss D:848-854) is a function of the per-image log-ratio
+Delta = lp_theta - lp_ref, i.e. of eps_pol - eps_ref.  The policy UNet runs in full-grad mode with save=True
+(trainer.py micro_step) and the frozen reference UNet with save=False; in torch both are the same module code, so their
+bf16 rounding is the same function of nearly the same weights and cancels in Delta.  Here the two passes must take the
+same kernel routes too: any difference in tile shape, epilogue or rounding point between them shows up as eps bits that
+differ on identical weights, and as bf16 noise that does not cancel in Delta (the round-3 C4-per-rank loss gap)."""
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+
+
+def _make(cuda, cfg):
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel
+    with torch.device(cuda):
+        u = UNet2DConditionModel(cfg)
+    u.init_weights(0)
+    return u
+
+
+def _inputs(cuda, B, h, seed=5):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(B, h, h, 4, device=cuda, generator=g).bfloat16()
+    t = torch.tensor([999.0, 749.0, 499.0, 249.0, 999.0, 499.0][:B] * (B // 6 + 1), device=cuda)[:B]
+    enc = torch.randn(B, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(B, 1280, device=cuda, generator=g).bfloat16()
+    tid = torch.tensor([[1024., 1024., 0., 0., 1024., 1024.]], device=cuda).repeat(B, 1)
+    return x, t, enc, pooled, tid
+
+
+def _caches(u):
+    """Every kernel-layout weight a forward reads, by a stable name."""
+    out = {}
+    for name, m in u.named_modules():
+        for attr in ("w_nhwc", "w_col", "w_mat", "w_qkv", "w_kv", "w_int", "b_int"):
+            t = getattr(m, attr, None)
+            if isinstance(t, torch.Tensor):
+                out[f"{name}.{attr}"] = t
+    out["_temb_w"], out["_temb_b"] = u._temb_w, u._temb_b
+    for C, grp in u._kv_groups.items():
+        out[f"kv_group_{C}"] = grp.W
+    return out
+
+
+@pytest.mark.parametrize("B", [6, 12])
+def test_full_policy_and_frozen_reference_same_bits(cuda, B):
+    """B = 6 (C3 window, P = 1) and 12 (C4 per-rank window, P = 2) images at 1024^2."""
+    from pairwise_sample_optimization_amd.unet import UNetConfig
+    cfg = UNetConfig.sdxl(128)
+    pol, ref = _make(cuda, cfg), _make(cuda, cfg)
+    fg = pol.enable_full_grads()
+    fg.master_from_params()
+    pol.prepare()
+    ref.prepare()
+    # the module parameters and every kernel-layout cache hold the same bits in both UNets
+    sp, sr = pol.state_dict(), ref.state_dict()
+    bad = [k for k in sp if not torch.equal(sp[k], sr[k])]
+    assert not bad, bad[:5]
+    cp, cr = _caches(pol), _caches(ref)
+    assert cp.keys() == cr.keys()
+    bad = [k for k in cp if not torch.equal(cp[k], cr[k])]
+    assert not bad, bad[:5]
+    # the fp32 master round-trips the bf16 working copy exactly
+    assert torch.equal(fg.master.bfloat16(), fg.work)
+    x, t, enc, pooled, tid = _inputs(cuda, B, 128)
+    with torch.no_grad():
+        e_ref, _ = ref.forward_nhwc(x, t, enc, pooled, tid, save=False)
+        e_pol_ns, _ = pol.forward_nhwc(x, t, enc, pooled, tid, save=False)
+    e_pol, rt = pol.forward_nhwc(x, t, enc, pooled, tid, save=True)
+    torch.cuda.synchronize()
+    nd = lambda a, b: int((a != b).sum().item())
+    print(f"B={B}: policy(save=True) vs reference differ in {nd(e_pol, e_ref)} of {e_ref.numel()} eps; "
+          f"policy(save=False) vs reference {nd(e_pol_ns, e_ref)}; policy save=True vs save=False "
+          f"{nd(e_pol, e_pol_ns)}")
+    assert torch.equal(e_pol_ns, e_ref)
+    assert torch.equal(e_pol, e_ref)
+    del rt

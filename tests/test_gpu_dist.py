@@ -30,5 +30,28 @@ def test_world2_trainer_step_bucketed_overlap(tmp_path):
         assert d["issued_before_finish"] == d["buckets"]  # every bucket left during the backward
         assert d["scale"] == 0.5
         assert d["grad_norm"] > 0
-        assert d["bucketed_vs_flat_rel"] < 1e-5           # float-atomic rounding of the dW kernels only
+        assert d["bucketed_vs_flat_rel"] == 0.0           # every reduction is ordered: same bits either way
         assert d["synced_equal_across_ranks"] and d["masters_equal_across_ranks"]
+
+
+def test_rccl_world1_bucketed_overlap_on_comm_stream(tmp_path):
+    """The product's RCCL path (init_process_group("nccl"), bench.py's backend) on the box's one GPU at world size 1:
+    RCCL still runs every collective on its own stream, so this exercises what the gloo tests cannot -- side.join()
+    before each async all_reduce with the side-stream LoRA dW kernels still in flight, work.wait() as a stream wait in
+    finish(), the bf16 wire cast back -- against the flat sync, bit for bit (tests/rccl_worker_gpu.py)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(HERE, "rccl_worker_gpu.py"), "--out", str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.load(open(os.path.join(tmp_path, "rank0.json")))
+    print(d)
+    assert d["backend"] == "nccl" and d["world"] == 1
+    assert d["buckets"] >= 8 and d["issued_before_finish"] == d["buckets"]
+    assert d["side_pending_at_issue"] > 0              # dW kernels were in flight on the side stream at some issue
+    assert d["grad_norm"] > 0
+    assert d["bucketed_equals_flat"] and d["wire_bf16_equals_cast"] and d["masters_equal"]

@@ -545,6 +545,49 @@ def test_tn_rank_batch_equals_individual_products(cuda):
         assert ((o2 - ref).norm() / ref.norm()).item() < 1e-3, (M, I, J, grp)
 
 
+def test_tn_rank_batch_deterministic(cuda):
+    """The training path's rank-r TN batch (pso_gemm_tn_rank_batch_ws: partials stored, added in row-range order) gives
+    the same bits on every run, also when two products of one launch accumulate into the same output (they go to
+    separate launches), and agrees with the f32-atomic form to rounding."""
+    from pairwise_sample_optimization_amd import kernels as K
+    assert K.TnRankQueue.deterministic
+    g = torch.Generator(device="cuda").manual_seed(22)
+    specs = [(16384, 1280, 32, 0), (16384, 32, 1280, 0), (8192, 3840, 96, 1280), (616, 64, 2048, 0),
+             (4000, 640, 64, 0), (32768, 640, 32, 0)]
+    ops = []
+    for M, I, J, grp in specs:
+        a = torch.randn(M, I, device=cuda, generator=g).bfloat16()
+        b = torch.randn(M, J, device=cuda, generator=g).bfloat16()
+        ops.append((a, b, grp, J * grp // I if grp else J))
+    shared = torch.zeros(1280, 32, device=cuda)
+    a2 = torch.randn(16384, 1280, device=cuda, generator=g).bfloat16()
+    b2 = torch.randn(16384, 32, device=cuda, generator=g).bfloat16()
+
+    def run(det):
+        K.TnRankQueue.deterministic = det
+        try:
+            outs = [torch.zeros(a.shape[1], r, device=cuda) for a, _, _, r in ops]
+            sh = shared.clone()
+            q = K.TnRankQueue()
+            for rep in range(2):
+                for (a, b, grp, _), o in zip(ops, outs):
+                    q.add(a, b, o, 0.5, group=grp)
+                q.add(a2, b2, sh, 1.0)
+                q.add(ops[0][0], ops[0][1], sh, 1.0)  # same output twice in one batch
+                q.flush()
+            torch.cuda.synchronize()
+            return outs + [sh]
+        finally:
+            K.TnRankQueue.deterministic = True
+
+    d1, d2, at = run(True), run(True), run(False)
+    for x, y, z in zip(d1, d2, at):
+        assert torch.equal(x, y)
+        assert ((x - z).norm() / z.norm()).item() < 1e-5
+    ref = 2 * (a2.float().t() @ b2.float() + ops[0][0].float().t() @ ops[0][1].float())
+    assert ((d1[-1] - ref).norm() / ref.norm()).item() < 1e-3
+
+
 @pytest.mark.parametrize("n", [2048 * 37, 2048 * 5 + 1003])
 def test_adamw8bit_vs_restatement(cuda, n):
     """pso_adamw8bit_step (bitsandbytes AdamW8bit, the reference's default optimizer T:427-435) against the numpy
@@ -585,3 +628,64 @@ def test_adamw8bit_vs_restatement(cuda, n):
     # it is an Adam step: against fp32 AdamW the parameters move the same way (codes cost a few % of the update)
     m, v = st.dequant()
     assert torch.isfinite(m).all() and (v >= 0).all()
+
+
+def test_adamw8bit_per_tensor_vs_restatement(cuda):
+    """pso_adamw8bit_step_blocks: bitsandbytes' per-tensor semantics on a flat buffer of mixed-size tensors (T:428-448,
+    ADVICE r3): blocks restart at every tensor, tensors under 4096 elements keep 32-bit state, alignment pads between
+    tensors are never touched, and non-finite gradient elements (injected at step 3) leave the parameter and its state
+    unchanged -- against oracle/adam8bit.adamw8bit_step_tensors over 5 steps (parity unpinned: no bitsandbytes)."""
+    import numpy as np
+    from oracle import adam8bit as O
+    from pairwise_sample_optimization_amd import kernels as K_
+    sizes = [5000, 1000, 4096, 4095, 20480, 64, 2049, 320]
+    segs, off = [], 0
+    for k in sizes:
+        segs.append((off, k))
+        off += -(-k // 64) * 64  # 64-element slots, as FullGradState lays the UNet parameters out
+    n = off
+    g_ = np.random.default_rng(4)
+    p = (g_.standard_normal(n) * 0.02).astype(np.float32)
+    pads = np.ones(n, bool)
+    for o, k in segs:
+        pads[o:o + k] = False
+    f32 = lambda x: float(np.float32(x))
+    lr, b1, b2, eps, wd = f32(1e-3), f32(0.9), f32(0.999), f32(1e-8), f32(1e-2)
+    pd = torch.tensor(p, device=cuda)
+    wb = torch.zeros(n, device=cuda, dtype=torch.bfloat16)
+    st = K_.Adam8State(n, cuda, segments=segs)
+    assert st.nblk == sum(-(-k // 2048) for k in sizes)
+    ost = {}
+    p0 = p.copy()
+    for step in range(1, 6):
+        # per-tensor gradient scales 1e-4 .. 1: a shared absmax would round the small tensors' state to code 0
+        gr = np.zeros(n, np.float32)
+        for i, (o, k) in enumerate(segs):
+            gr[o:o + k] = g_.standard_normal(k).astype(np.float32) * np.float32(10.0 ** (-(i % 5)))
+        if step == 3:
+            gr[[3, 5001, 7000, 12000]] = [np.nan, np.inf, -np.inf, np.nan]
+        K_.adamw8bit_step(pd, torch.tensor(gr, device=cuda), st, lr, (b1, b2), eps, wd, step, out_bf16=wb)
+        p = O.adamw8bit_step_tensors(p, gr, segs, ost, lr, b1, b2, eps, wd, step)
+    torch.cuda.synchronize()
+    pk = pd.cpu().numpy()
+    assert np.isfinite(pk).all()
+    assert np.array_equal(pk[pads], p0[pads])                       # pads untouched
+    assert np.abs(pk - p).max() <= 1e-6 * np.abs(p).max()
+    qm, qv = st.qm.cpu().numpy(), st.qv.cpu().numpy()
+    am, av = st.am.cpu().numpy(), st.av.cpu().numpy()
+    m32, v32 = st.m32.cpu().numpy(), st.v32.cpu().numpy()
+    for b, (o, k, so, _) in enumerate(st.rows):
+        seg_off = max(so_ for so_, _ in segs if so_ <= o)
+        ref = ost[seg_off]
+        if so >= 0:  # 32-bit tensor (one block: k < 4096 < 2 * 2048 only when k <= 2048; else two)
+            r0 = o - seg_off
+            assert np.allclose(m32[so:so + k], ref["m32"][r0:r0 + k], rtol=1e-6, atol=1e-12)
+            assert np.allclose(v32[so:so + k], ref["v32"][r0:r0 + k], rtol=1e-6, atol=1e-14)
+        else:
+            bi = (o - seg_off) // 2048
+            assert am[b] == ref["am"][bi] and av[b] == ref["av"][bi], (b, o)
+            r0 = o - seg_off
+            assert (qm[o:o + k] == ref["qm"][r0:r0 + k]).mean() > 0.999
+            assert (qv[o:o + k] == ref["qv"][r0:r0 + k]).mean() > 0.999
+    keep = torch.tensor(~pads, device=cuda)
+    assert torch.equal(wb[keep], pd.bfloat16()[keep])  # the fused bf16 working copy (pads: never written)
