@@ -124,6 +124,16 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
              int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
              int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
              int tail_group_n, int tail_rows, void* stream);
+/* pso_gemm with a caller-owned fp32 workspace: dense products whose output tiles leave most CUs idle while the
+ * reduction is long (M x N <= 128 tiles of 128 x 160, K >= 2048: the bs = 1 backward at M = 2048) split K over
+ * workgroups; every split STORES its partial into ws and a second kernel adds them in split order and applies the
+ * epilogue (deterministic, no atomics).  pso_gemm_ws_bytes(M, N, K1, K2) = the workspace that needs (0: no split);
+ * any other shape or a smaller workspace runs as pso_gemm. */
+size_t pso_gemm_ws_bytes(int M, int N, int K1, int K2);
+int pso_gemm_ws(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
+                int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+                int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
+                int tail_group_n, int tail_rows, void* ws, size_t ws_bytes, void* stream);
 
 /* Batched dense product out_z[M][N] = alpha * A_z[M][K] . B_z[N][K]^T for z < batch, operand z at z * stride_* elements
  * (bf16 A/B, bf16 or f32 out).  Replaces the per-image loop of the VAE mid-block attention (diffusers Attention with

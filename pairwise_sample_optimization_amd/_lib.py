@@ -51,6 +51,9 @@ SIGNATURES = {
     "pso_db_loss_bwd": (ci, [ci, ci, ci, vp, ci, vp, vp, vp, cf, cf, cf, vp, cf, vp, ci, vp, csz, vp]),
     "pso_gemm": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                       ci, ci, vp]),
+    "pso_gemm_ws_bytes": (csz, [ci, ci, ci, ci]),
+    "pso_gemm_ws": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
+                         ci, ci, vp, csz, vp]),
     "pso_gemm_batched": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, ci, vp]),
     "pso_gemm_set_variant": (None, [ci]),
     "pso_last_kernel": (ctypes.c_char_p, []),

@@ -59,6 +59,9 @@ struct GemmArgs {
   // batched form (gridDim.z = batch, dense A only): operand z starts batch strides further on (elements)
   long bat_a, bat_b, bat_o;
   int batch;
+  // deterministic split-K (gridDim.y > 1 with ws): every split STORES its raw partial acc into ws[split][M][N]
+  // (fp32, row pitch N); gemm_splitk_reduce_kernel adds the splits in order and applies the epilogue
+  float* ws;
 };
 
 #define EPI_NONE 0
@@ -442,6 +445,24 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
   }  // !PIPE
 
   // ---- epilogue: lane holds out[m][n0..n0+3] for each (i, j) ----
+  if constexpr (EPI == EPI_NONE && !PIPE) {
+    if (g.ws) {  // deterministic split-K: this split's partial product (every split stores, empty ones zeros)
+      float* part = g.ws + (long)blockIdx.y * g.M * g.N;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + fr;
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = n0 + wn * (BN / WN) + j * 16 + fk * 4;
+          if (n < g.N)
+            *reinterpret_cast<float4*>(part + (long)m * g.N + n) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                                                                              acc[i][j][3]);
+        }
+      }
+      return;
+    }
+  }
   if constexpr (EPI == EPI_GEGLU) {
     // this wave's 64 columns = one interleaved group: subtiles j = 0,1 hold h, j = 2,3 the matching gate columns.
     // h and gate are rounded to bf16 first (the unfused path stores them in bf16 before the GEGLU).
@@ -781,6 +802,64 @@ int pso_gemm8p320_geglu_bwd_run(int M, int N, int K, const void* a, long lda, co
                                 long ldaux, void* out, long ldo, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
+// Ordered reduction of the split-K partials + the plain epilogue (4 consecutive columns per thread, N % 4 == 0):
+//   y = alpha * sum_s ws[s][m][n] + bias[n] + rowbias[m / rows_per_group][n]
+//   bf16 out: out = bf16(bf16(y) + resid) (the staged epilogue's rounding: the residual is added to the rounded
+//             projection, as the unfused Linear + add does), f32 out: out (+)= y + resid
+__global__ void gemm_splitk_reduce_kernel(GemmArgs g, int ks) {
+  const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int nq = g.N / 4;
+  if (q >= (long)g.M * nq) return;
+  const int m = (int)(q / nq), n = (int)(q - (long)m * nq) * 4;
+  const float* src = g.ws + (long)m * g.N + n;
+  float4 acc = *reinterpret_cast<const float4*>(src);
+  for (int s = 1; s < ks; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(src + (long)s * g.M * g.N);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  float v[4] = {acc.x * g.alpha, acc.y * g.alpha, acc.z * g.alpha, acc.w * g.alpha};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (g.bias) v[r] += bf2f(g.bias[n + r]);
+    if (g.rowbias) v[r] += bf2f(g.rowbias[(long)(m / g.rows_per_group) * g.ld_rowbias + n + r]);
+  }
+  if (g.out_dtype == PSO_BF16) {
+    if (g.resid) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(g.resid[(long)m * g.ldr + n + r]);
+    }
+    bf16_t* o = reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n;
+    *reinterpret_cast<uint2*>(o) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+  } else {
+    float* o = reinterpret_cast<float*>(g.out) + (long)m * g.ldo + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (g.resid) v[r] += bf2f(g.resid[(long)m * g.ldr + n + r]);
+      o[r] = g.accumulate ? o[r] + v[r] : v[r];
+    }
+  }
+}
+
+// Split-K plan of a dense GEMM whose output tiles leave most CUs idle while its reduction is long (the bs = 1 / GPU
+// backward at M = 2048: 2048 x 1280 x 10240 makes 128 tiles of 128 x 160 -- half a 256-CU round at one workgroup
+// each): ks K-splits of >= 16 K-tiles each, towards 512 workgroups (two per CU), reduced in split order through a
+// caller-owned fp32 workspace (deterministic).  The partials cost 8 M N bytes per split against 2 M N K / ks flop,
+// so only K >= 2048 qualifies.  Returns ks (0: no split) and the tile.
+struct SplitPlan { int ks, bm, bn; };
+static SplitPlan gemm_split_plan(int M, int N, int K1, int K2, bool has_tail, bool dense) {
+  SplitPlan p{0, 0, 0};
+  if (!dense || M <= 0 || N <= 0 || (N % 4) != 0) return p;
+  const int bm = 128, bn = (N % 160) == 0 ? 160 : 128;
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int nt_all = (K1 + 63) / 64 + (has_tail ? (K2 + 63) / 64 : 0);
+  if (tiles > 128 || nt_all < 32) return p;
+  int ks = (int)((512 + tiles - 1) / tiles);
+  if (ks > nt_all / 16) ks = nt_all / 16;
+  if (ks < 2) return p;
+  p.ks = ks; p.bm = bm; p.bn = bn;
+  return p;
+}
+
 static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
@@ -795,7 +874,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
   const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
-                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47)
+                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47 || gv_raw == 48 || gv_raw == 49)
                      ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
@@ -818,6 +897,18 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
     if ((g.N % 160) == 0 && tl(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
     if (tl(128, 128) >= 256) return launch<128, 128, 2, 4, 2>(g, st);
     return launch<64, 64>(g, st);
+  }
+  // deterministic split-K through the caller's workspace (pso_gemm_ws): small M x N, long K
+  if (g.ws) {
+    const SplitPlan sp = gemm_split_plan(g.M, g.N, g.K1, g.K2, g.a2 != nullptr, !g.conv.mode);
+    if (sp.ks >= 2) {
+      if (sp.bn == 160) launch<128, 160, 2, 2, 2>(g, st, sp.ks);
+      else launch<128, 128, 2, 4, 2>(g, st, sp.ks);
+      const long n4 = (long)g.M * (g.N / 4);
+      gemm_splitk_reduce_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(g, sp.ks);
+      return pso_check_launch("pso_gemm_ws");
+    }
+    g.ws = nullptr;
   }
   // Skinny N (the LoRA rank-r products): one 16-row x all-N tile per 4-wave block, K split over the waves.
   if (gv == 0 && !g.conv.mode && !g.a2 && !g.bias && !g.rowbias && !g.resid && g.N <= 128 &&
@@ -923,6 +1014,10 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (gv == 17 && n320) return launch<128, 320, 2, 4, 2>(g, st);
   if (gv == 18 && n320) return launch<256, 320, 2, 4, 2>(g, st);
   if (gv == 19 && n160) return launch<128, 160, 2, 2, 2, true>(g, st);
+  // small-M tiles (the bs = 1 backward at M = 2048: N = 1280 makes exactly one 256-CU round of 64 x 160 / 128 x 80)
+  if (gv == 20 && n160) return launch<64, 160, 2, 2, 2>(g, st);
+  if (gv == 21 && (g.N % 80) == 0 && (g.tail_group_n % 80) == 0) return launch<128, 80, 4, 1, 2>(g, st);
+  if (gv == 22 && n160) return launch<64, 160, 2, 2, 3>(g, st);
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).
@@ -947,6 +1042,16 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (gv_raw != 46 && !bn64_only && n160 && tiles(128, 160) >= 384 && tiles(128, 160) < 512 &&
       tiles(128, 128) <= 512)
     return launch<128, 128, 2, 4, 2>(g, st);
+  // 128 x 160 tiles that make at most one workgroup per CU while 64 x 160 ones make 1.5-2 (the bs = 1 / GPU pass:
+  // 4096 x 1280 and 8192 x 640 rows; tools/small_m_bench.py, one box: 4096 x 1280 x 5120 837 vs 755 TF/s, x 1280 + LoRA
+  // 649 vs 540, 8192 x 640 x 5120 843 vs 759, x 1920 + LoRA 718 vs 637); variant 48 keeps 128 x 160 there
+  if (gv_raw != 48 && n160 && tiles(128, 160) <= 256 && tiles(64, 160) >= 384) return launch<64, 160, 2, 2, 2>(g, st);
+  // smaller still (M = 2048, N = 1280: 256 tiles of 64 x 160, 640 of 64 x 64), short K (the long ones split K through
+  // a workspace, pso_gemm_ws): the register-pipelined 8-wave 128 x 128 tiles (tools/small_m_bench.py: 2048 x 1280 x
+  // 1280 + LoRA 404 vs 319 TF/s for 64 x 64); variant 49 keeps 64 x 64 there
+  if (gv_raw != 49 && !g.conv.mode && !bn64_only && (g.N % 128) == 0 && tiles(64, 160) <= 256 &&
+      tiles(128, 128) >= 128 && tiles(128, 160) < 256)
+    return launch<128, 128, 2, 4, 2, true>(g, st);
   if (n160 && tiles(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
   if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= (g.conv.mode ? 128 : 256))
     return launch<256, 256, 2, 4, 2>(g, st);
@@ -1342,6 +1447,47 @@ int pso_gemm(int M, int N, const void* a1, long lda1, int K1, const void* b1, lo
   g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  return run_gemm(g, (hipStream_t)stream);
+}
+
+size_t pso_gemm_ws_bytes(int M, int N, int K1, int K2) {
+  const SplitPlan sp = gemm_split_plan(M, N, K1, K2, K2 > 0, true);
+  return sp.ks >= 2 ? (size_t)sp.ks * M * N * sizeof(float) : 0;
+}
+
+int pso_gemm_ws(int M, int N, const void* a1, long lda1, int K1, const void* b1, long ldb1, const void* a2, long lda2,
+                int K2, const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+                int rows_per_group, const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate,
+                int tail_group_n, int tail_rows, void* ws, size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && N >= 0 && K1 >= 0 && (K1 % 8) == 0, "pso_gemm_ws: need K1 %% 8 == 0 (K1=%d)", K1);
+  PSO_ARG_CHECK(a1 && b1 && out, "pso_gemm_ws: null operand");
+  PSO_ARG_CHECK(al16(a1) && al16(b1) && (lda1 % 8) == 0 && (ldb1 % 8) == 0, "pso_gemm_ws: A1/B1 must be 16-B aligned rows");
+  PSO_ARG_CHECK(!a2 || (b2 && (K2 % 8) == 0 && al16(a2) && al16(b2) && (lda2 % 8) == 0 && (ldb2 % 8) == 0),
+                "pso_gemm_ws: bad second operand");
+  PSO_ARG_CHECK(out_dtype == PSO_BF16 || out_dtype == PSO_F32, "pso_gemm_ws: bad out dtype");
+  PSO_ARG_CHECK((long)M * lda1 < 0x7fffffffL && (long)N * ldb1 < 0x7fffffffL,
+                "pso_gemm_ws: operand spans more than 2^31 elements");
+  PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_gemm_ws: accumulate needs f32 output");
+  PSO_ARG_CHECK(!rowbias || rows_per_group > 0, "pso_gemm_ws: rowbias needs rows_per_group > 0");
+  GemmArgs g{};
+  g.a1 = (const bf16_t*)a1; g.lda1 = lda1; g.K1 = K1;
+  g.b1 = (const bf16_t*)b1; g.ldb1 = ldb1;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
+  g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
+  g.tail_group_n = a2 ? tail_group_n : 0;
+  g.tail_m = (tail_rows > 0 && tail_rows < M) ? tail_rows : M;
+  g.M = M; g.N = N;
+  g.alpha = alpha;
+  g.bias = (const bf16_t*)bias;
+  g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
+  g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  // the workspace form applies when the plan splits and the caller's workspace holds every split; else pso_gemm
+  const SplitPlan sp = gemm_split_plan(M, N, K1, a2 ? K2 : 0, a2 != nullptr, true);
+  const bool ok = ws && (((uintptr_t)ws) & 15) == 0 && sp.ks >= 2 && ws_bytes >= (size_t)sp.ks * M * N * sizeof(float) &&
+                  (ldo % 4) == 0 && (out_dtype == PSO_F32 ? al16(out) : al8(out)) && (g.tail_group_n % sp.bn) == 0 &&
+                  g_gemm_variant == 0;
+  g.ws = ok ? (float*)ws : nullptr;
   return run_gemm(g, (hipStream_t)stream);
 }
 

@@ -88,6 +88,9 @@ def _row_stride(t):
     return t.stride(0)
 
 
+_GEMM_WS = {}  # (M, N, K1, K2) -> pso_gemm_ws_bytes
+
+
 def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=None, rows_per_group=1, out=None,
          out_dtype=BF16, accumulate=False, tail_group_n=0, tail_rows=0):
     """out[M,N] = alpha*(a @ w^T + a2 @ w2^T) + bias + rowbias[m // rows_per_group] + resid.
@@ -104,14 +107,22 @@ def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=No
         assert a2.shape[1] == (K2 * (N // tail_group_n) if tail_group_n else K2)
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=out_dtype)
+    key = (M, N, K1, K2)
+    wsb = _GEMM_WS.get(key)
+    if wsb is None:
+        wsb = _GEMM_WS[key] = int(lib().pso_gemm_ws_bytes(M, N, K1, K2))
+    args = (M, N, ptr(a), _row_stride(a), K1, ptr(w), _row_stride(w),
+            ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
+            ptr(w2), _row_stride(w2) if w2 is not None else 0,
+            float(alpha), ptr(bias), ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
+            int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
+            ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n), int(tail_rows))
     e0 = _prof_begin()
-    check(lib().pso_gemm(M, N, ptr(a), _row_stride(a), K1, ptr(w), _row_stride(w),
-                         ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
-                         ptr(w2), _row_stride(w2) if w2 is not None else 0,
-                         float(alpha), ptr(bias), ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
-                         int(rows_per_group), ptr(resid), _row_stride(resid) if resid is not None else 0,
-                         ptr(out), _row_stride(out), dtype_code(out), int(accumulate), int(tail_group_n),
-                         int(tail_rows), stream_ptr()), "pso_gemm")
+    if wsb:  # small M x N, long K: deterministic split-K through a workspace (pso_gemm_ws)
+        ws = torch.empty(wsb, device=a.device, dtype=torch.uint8)
+        check(lib().pso_gemm_ws(*args, ptr(ws), wsb, stream_ptr()), "pso_gemm_ws")
+    else:
+        check(lib().pso_gemm(*args, stream_ptr()), "pso_gemm")
     _prof_end(e0, 2.0 * M * N * K1 + 2.0 * (tail_rows if 0 < tail_rows < M else M) * N * K2,
               2.0 * (M * (K1 + (a2.shape[1] if a2 is not None else 0)) + N * (K1 + K2)) + out.element_size() * M * N,
               ("gemm", M, N, K1, K2, tail_group_n, out.dtype == torch.float32))
@@ -260,6 +271,11 @@ def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
     J = b.shape[1]
     r = J * group // I if group else J
     assert b.shape[0] == M and out.shape == (I, r) and out.dtype == torch.float32
+    if split_ws and TnRankQueue.deterministic and _tn_rank_form(a, b, group) is not None:
+        q = TnRankQueue()  # a rank-r product (grouped or not): the ordered workspace form, issued at once
+        q.add(a, b, out, alpha, group)
+        q.flush()
+        return out
     e0 = _prof_begin()
     wsb = lib().pso_gemm_tn_ws_bytes(M, I, J) if group == 0 and split_ws else 0
     if wsb:  # full-weight gradient with few 128 x 128 tiles: split rows, ordered reduction through a workspace
@@ -271,6 +287,19 @@ def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
                                         ptr(out), _row_stride(out), int(group), stream_ptr()), "pso_gemm_tn")
     _prof_end(e0, 2.0 * M * I * r, 2.0 * M * (I + J) + 8.0 * I * r, ("gemm_tn", M, I, J, group))
     return out
+
+
+def _tn_rank_form(a, b, group):
+    """(key, x, u, R, group_c) of a TN product gemm_tn(a, b, ...) that the rank-r streaming kernel takes, else None:
+    x the >= 128-wide side, u the rank-R side, key = (R, out_jc)."""
+    I, J = a.shape[1], b.shape[1]
+    r = J * group // I if group else J
+    rk = lambda v: v in TN_RANKS
+    if I % 128 == 0 and (rk(J) if group == 0 else (group % 128 == 0 and I % group == 0 and rk(r))):
+        return (r, 0), a, b, r, group
+    if J % 128 == 0 and group == 0 and rk(I):
+        return (I, 1), b, a, I, 0
+    return None
 
 
 class TnRankQueue:
@@ -292,13 +321,10 @@ class TnRankQueue:
         J = b.shape[1]
         r = J * group // I if group else J
         assert b.shape[0] == M and out.shape == (I, r) and out.dtype == torch.float32
-        rk = lambda x: x in TN_RANKS
-        if I % 128 == 0 and (rk(J) if group == 0 else (group % 128 == 0 and I % group == 0 and rk(r))):
-            key, x, u, R, gc = (r, 0), a, b, r, group
-        elif J % 128 == 0 and group == 0 and rk(I):
-            key, x, u, R, gc = (I, 1), b, a, I, 0
-        else:
+        form = _tn_rank_form(a, b, group)
+        if form is None:
             return gemm_tn(a, b, out, alpha, group)
+        key, x, u, R, gc = form
         require_cuda(x, u, out)
         prob = _lib.PsoTnRankProblem(ptr(x), _row_stride(x), ptr(u), _row_stride(u), ptr(out), _row_stride(out),
                                      M, x.shape[1], gc, float(alpha))

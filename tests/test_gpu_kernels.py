@@ -193,9 +193,10 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 30, 31, 37, 38, 41])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 20, 21, 22, 30, 31, 37,
+                                     38, 41, 48, 49])
 @pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
-                                        (8192, 640, 320, 0), (1000, 700, 136, 0)])
+                                        (8192, 640, 320, 0), (1000, 700, 136, 0), (2048, 1280, 1280, 1280)])
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
     """Every tile configuration on UNet-scale shapes, with and without the grouped LoRA K-tail (3 groups)."""
     from pairwise_sample_optimization_amd import kernels as K_
@@ -222,6 +223,49 @@ def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
         assert (sentinel[M:] == 7.0).all()  # nothing written past the output
     finally:
         K_.lib().pso_gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("M,N,K,K2,tail_rows,f32", [(2048, 1280, 10240, 0, 0, False), (2048, 1280, 3840, 96, 0, False),
+                                                    (2000, 1280, 4096, 32, 1000, False), (1024, 640, 5120, 0, 0, True),
+                                                    (2048, 1280, 2560, 32, 0, True)])
+def test_gemm_splitk_workspace(cuda, M, N, K, K2, tail_rows, f32):
+    """pso_gemm_ws (the bs = 1 backward's small-M, long-K products): split-K through a workspace, the splits added in
+    order by a second kernel that applies the epilogue -- bias, row-group bias or residual, bf16 or f32 (accumulate)
+    output, the LoRA K-tail on the first tail_rows rows -- against fp32, bit-identical on a second run."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    assert K_.lib().pso_gemm_ws_bytes(M, N, K, K2) > 0  # the shape takes the split path
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda, generator=g).bfloat16()
+    r = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    kw = {}
+    ref = a.float() @ w.float().t() * 0.5
+    if K2:
+        rows = tail_rows or M
+        u = torch.randn(rows, K2, device=cuda, generator=g).bfloat16()
+        w2 = (torch.randn(N, K2, device=cuda, generator=g) / 6).bfloat16()
+        kw = dict(a2=u, w2=w2, tail_rows=tail_rows)
+        ref[:rows] += 0.5 * (u.float() @ w2.float().t())
+    if f32:
+        base = torch.randn(M, N, device=cuda, generator=g)
+        outs = []
+        for _ in range(2):
+            o = base.clone()
+            K_.gemm(a, w, bias=b, alpha=0.5, out=o, out_dtype=torch.float32, accumulate=True, **kw)
+            outs.append(o)
+        ref = base + ref + b.float()
+        assert _rel(outs[0], ref) < 1e-5
+    else:
+        outs = []
+        for _ in range(2):
+            sentinel = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+            K_.gemm(a, w, bias=b, resid=r, alpha=0.5, out=sentinel[:M], **kw)
+            assert (sentinel[M:] == 7.0).all()
+            outs.append(sentinel[:M])
+        ref = ref + b.float() + r.float()
+        assert _rel(outs[0], ref) < 4e-3
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 1280), (1000, 768, 640), (300, 256, 128), (16384, 1024, 256),
