@@ -562,7 +562,10 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, i
 // as the A operand -> lane holds S[q = 4g + r][k = c]; P and dS then feed dV^T += dO^T P and dK^T += Q^T dS as
 // lane-local B operands (query order permuted inside each 32-deep step, matching the transposed dO / Q reads).
 // ================================================================================================================
-template <int KJ, int STG>
+// PF: the tile's 64 LSE / -delta values are read into registers once, right after the tile's barrier (8 ds_read_b128
+// behind one lgkmcnt wait), instead of one read + wait + scheduling barrier per 16-query subtile -- so nothing pins the
+// S / dP MFMAs of one subtile behind the exp / dS vector work of the previous one
+template <int KJ, int STG, bool PF = false>
 __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a, int nkb) {
   constexpr int IMG = ATT_KT * ATT_D;  // elements of one 64 x 64 image
   constexpr int PIECES = 8;            // 16-B glds per wave per tile (+1 dword piece on waves 0 and 1)
@@ -665,6 +668,16 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
     const float* sD = sL + 64;
     const int qbase = (qa + i) * ATT_KT;
     const bool qpart = qbase + ATT_KT > a.Sq;
+    float4 lpf[4], dpf[4];
+    if constexpr (PF) {
+#pragma unroll
+      for (int qs = 0; qs < 4; ++qs) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(lpf[qs]) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sL + qs * 16 + 4 * g)));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(dpf[qs]) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int qk = 0; qk < 2; ++qk) {
       // P and dS for 32 queries (2 subtiles) x this wave's keys: lane holds X[q = qs*16 + 4g + r][k = kj*16 + c]
@@ -681,10 +694,15 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         // LSE / delta through inline-asm LDS reads: as plain loads hipcc cannot tell them from the ring's pending
         // LDS-DMA writes and drains the whole ring (vmcnt(0)), prefetch of the next query tile included
         float4 l4, d4;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(l4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sL + qs * 16 + 4 * g)));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(d4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);  // nothing reads l4 / d4 (or moves above) before the wait
+        if constexpr (PF) {
+          l4 = lpf[qs];
+          d4 = dpf[qs];
+        } else {
+          asm volatile("ds_read_b128 %0, %1" : "=v"(l4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sL + qs * 16 + 4 * g)));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(d4) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);  // nothing reads l4 / d4 (or moves above) before the wait
+        }
         float lq[4] = {l4.x, l4.y, l4.z, l4.w};  // LSE * log2(e), from the dQ kernel
         const f32x4 ndel = {d4.x, d4.y, d4.z, d4.w};  // -delta, from the dQ kernel
         if (qpart) {
@@ -1087,9 +1105,12 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
       attr4 = true;
     }
     attn_bwd_dkv_kernel<4, 3><<<nkb4 * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb4);
-  } else {
+  } else if (g_attn_bwd_variant == 1) {  // per-subtile LSE / delta reads (the round-3 form, A/B knob)
     const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
     attn_bwd_dkv_kernel<2, 2><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
+  } else {  // tile-level LSE / delta prefetch: L1 self-attention backward 1.156-1.179 vs 1.188-1.233 ms
+    const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    attn_bwd_dkv_kernel<2, 2, true><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
   }
   if (qsplit > 1) {
     // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)

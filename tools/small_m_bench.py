@@ -66,8 +66,10 @@ def main():
             except Exception as e:  # variant not applicable to the shape
                 line += f"{'-':>8} "
         K.lib().pso_gemm_set_variant(0)
+        K.gemm(a, w, **kw)
+        kname = K.lib().pso_last_kernel().decode().replace("gemm_bf16_kernel", "2p").replace("gemm8p_kernel", "8p")
         wt = w.t()
-        line += f"{fl / t_ms(lambda: torch.mm(a, wt)) / 1e9:10.0f}"
+        line += f"{fl / t_ms(lambda: torch.mm(a, wt)) / 1e9:10.0f}   v0: {kname}"
         print(line, flush=True)
 
 
