@@ -728,15 +728,35 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
       }
       // dV^T[d][k] += dO^T . P ;  dK^T[d][k] += Q^T . dS
       bf16x8 of[4], qf[4];
+      if constexpr (PF) {
+        // the wait is tied to the 16 read registers (no scheduling barrier): only the dV / dK MFMAs wait for it, so
+        // the compiler may interleave them with the next subtile's independent work
+        s16x4 otr[8], qtr[8];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        of[dt] = cat_frag(tr_read_asm(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
-                          tr_read_asm(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
-        qf[dt] = cat_frag(tr_read_asm(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
-                          tr_read_asm(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+        for (int dt = 0; dt < 4; ++dt) {
+          otr[2 * dt] = tr_read_asm(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane);
+          otr[2 * dt + 1] = tr_read_asm(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane);
+          qtr[2 * dt] = tr_read_asm(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane);
+          qtr[2 * dt + 1] = tr_read_asm(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane);
+        }
+        lds_wait8(otr);
+        lds_wait8(qtr);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          of[dt] = cat_frag(otr[2 * dt], otr[2 * dt + 1]);
+          qf[dt] = cat_frag(qtr[2 * dt], qtr[2 * dt + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          of[dt] = cat_frag(tr_read_asm(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
+                            tr_read_asm(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+          qf[dt] = cat_frag(tr_read_asm(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane),
+                            tr_read_asm(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll

@@ -874,7 +874,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
   // off / forced
   const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
-                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47 || gv_raw == 48 || gv_raw == 49)
+                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47 || gv_raw == 48 || gv_raw == 49 || gv_raw == 50)
                      ? 0 : gv_raw;
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
@@ -963,7 +963,12 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   const long t320w = (long)((g.M + 255) / 256) * (g.N / 320);
   const bool wide320 = gv == 0 && gv_raw != 46 && ok320w && g.N >= 2560 && (t256 % 256) != 0 && t320w >= 256 &&
                        (t320w % 256) == 0;
-  if (ok8 && !wide320 && (gv == 30 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
+  // three quarters of a round of 256 x 256 tiles where the 256 x 320 ones leave more CUs idle (C4's 12288 x 1280:
+  // 240 vs 192 tiles, 1056 vs 877-919 TF/s; bs = 1's q/k/v 4096 x 3840: 240 tiles, 938 vs 798 on the 2-phase
+  // tiles; tools/small_m_bench.py); variant 50 keeps the full-round rule
+  const long t320r = (g.N % 320) == 0 ? (long)((g.M + 255) / 256) * (g.N / 320) : 0;
+  const bool part256 = gv == 0 && gv_raw != 50 && t256 >= 192 && t256 < 256 && t256 > t320r;
+  if (ok8 && !wide320 && (gv == 30 || part256 || ((gv == 32 || (gv == 0 && g.N >= 2560)) && t256 >= 256)))
     return pso_gemm8p_run(0, g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                           g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, nullptr, 0, 0, nullptr, 0,
                           g.group_m, st);

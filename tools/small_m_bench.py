@@ -10,6 +10,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pairwise_sample_optimization_amd import kernels as K  # noqa: E402
 
+C3_SHAPES = [  # the full-UNet step at 6 images (BASELINE C3): L2 M = 6144, L1 M = 24576, no LoRA tail
+    (6144, 1280, 1280, 0, 0), (6144, 1280, 5120, 0, 0), (6144, 3840, 1280, 0, 0), (6144, 1280, 10240, 0, 0),
+    (6144, 5120, 1280, 0, 0), (24576, 640, 640, 0, 0), (24576, 640, 2560, 0, 0), (24576, 1920, 640, 0, 0),
+    (24576, 640, 5120, 0, 0), (12288, 1280, 1280, 0, 0), (12288, 1280, 5120, 0, 0),
+]
 SHAPES = [  # (M, N, K, K2 LoRA tail, tail_rows)  from gpurun_out/shp.log (bs = 1)
     (2048, 1280, 10240, 0, 0), (2048, 1280, 1280, 32, 0), (2048, 1280, 3840, 96, 0), (4096, 1280, 1280, 32, 2048),
     (4096, 1280, 5120, 0, 0), (4096, 3840, 1280, 32, 2048), (8192, 640, 5120, 0, 0), (16384, 640, 640, 32, 8192),
@@ -38,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     torch.manual_seed(0)
     ops = []
-    for M, N, Kd, K2, tr in SHAPES:
+    for M, N, Kd, K2, tr in (C3_SHAPES if os.environ.get("GEMM_C3") else SHAPES):
         a = torch.randn(M, Kd, device=dev).bfloat16()
         w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).bfloat16()
         kw = {}
