@@ -1602,8 +1602,10 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
     return pso_gemm8p320_geglu_bwd_run(M, N, K, a, lda, w, ldw, pre, ld_pre, out, ldo, g.group_m, st);
   // 8-phase form (staggered wave groups) by default: 716 vs 658 TF/s for the 2-phase 128x160 kernel at
   // 16384 x 5120 x 1280, 489 vs 472 at 65536 x 2560 x 640 (tools/gemm_bench.py, one box); variant 31 keeps 128x160
+  // (from two rounds of tiles: below that the 2-phase 128 x 160 tiles with two workgroups per CU win -- bs = 1's
+  // 2048 x 5120 x 1280 620 vs 493-522 TF/s, C3's 6144 x 5120 x 1280 719 vs 680; tools/small_m_bench.py GEGLU_BWD=1)
   if (g_gemm_variant != 31 && (N % 256) == 0 && (K % 64) == 0 && fits30(M, lda) &&
-      fits30(N, ldw) && (long)((M + 255) / 256) * (N / 256) >= 128)
+      fits30(N, ldw) && (long)((M + 255) / 256) * (N / 256) >= 512)
     return pso_gemm8p_run(2, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, nullptr, nullptr, 0, out,
                           ldo, nullptr, 0, 0, pre, ld_pre, g.group_m, st);
   const long t160 = (long)((M + 127) / 128) * ((N + 159) / 160);

@@ -35,8 +35,29 @@ def t_ms(fn, it=30):
     return e0.elapsed_time(e1) / it
 
 
+def geglu_bwd(dev, variants):
+    """The fused GEGLU backward GEMM (dout = dy W_out^T, interleaved input gradient from the saved pre-activation) on
+    the bs = 1 / C2 / C3 shapes."""
+    print("geglu_bwd".ljust(34) + "".join(f"{'v' + str(v):>9}" for v in variants))
+    for M, F, Kd in [(2048, 5120, 1280), (8192, 2560, 640), (8192, 5120, 1280), (32768, 2560, 640), (6144, 5120, 1280),
+                     (24576, 2560, 640)]:
+        dy = torch.randn(M, Kd, device=dev).bfloat16()
+        wt = (torch.randn(F, Kd, device=dev) / Kd ** 0.5).bfloat16()
+        pre = torch.randn(M, 2 * F, device=dev).bfloat16()
+        line = f"{M}x{F}x{Kd}".ljust(34)
+        for v in variants:
+            K.lib().pso_gemm_set_variant(v)
+            ms = t_ms(lambda: K.gemm_geglu_bwd(dy, wt, pre))
+            line += f"{2 * M * F * Kd / ms / 1e9:8.0f} "
+        K.lib().pso_gemm_set_variant(0)
+        print(line, flush=True)
+
+
 def main():
     dev = torch.device("cuda")
+    if os.environ.get("GEGLU_BWD"):
+        variants = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,0,31,45").split(",")]
+        return geglu_bwd(dev, variants)
     x = torch.randn(8192, 8192, device=dev).bfloat16()
     for _ in range(200):
         x @ x
