@@ -869,13 +869,13 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
+// the variants 37-50 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// 256 x 160 8-phase tiles off / forced; ...); any other non-zero variant forces one tile shape
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 50) ? 0 : gv_raw; }
+
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
-  // 41 = automatic dispatch with the per-lane epilogue; 37 / 38 = automatic dispatch with the 256 x 160 8-phase tiles
-  // off / forced
-  const int gv = (gv_raw == 41 || gv_raw == 37 || gv_raw == 38 || gv_raw == 39 || gv_raw == 40 || gv_raw == 42 ||
-                  gv_raw == 43 || gv_raw == 44 || gv_raw == 45 || gv_raw == 46 || gv_raw == 47 || gv_raw == 48 || gv_raw == 49 || gv_raw == 50)
-                     ? 0 : gv_raw;
+  const int gv = gemm_auto_variant(gv_raw);
   if (g.M <= 0 || g.N <= 0) return PSO_OK;
   g.group_m = g_gemm_group > 0 ? g_gemm_group : PSO_GEMM_GROUP_M;
   if (g.tail_group_n > 0 && (g.tail_group_n % 64) != 0) {
@@ -1052,9 +1052,10 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // 649 vs 540, 8192 x 640 x 5120 843 vs 759, x 1920 + LoRA 718 vs 637); variant 48 keeps 128 x 160 there
   if (gv_raw != 48 && n160 && tiles(128, 160) <= 256 && tiles(64, 160) >= 384) return launch<64, 160, 2, 2, 2>(g, st);
   // smaller still (M = 2048, N = 1280: 256 tiles of 64 x 160, 640 of 64 x 64), short K (the long ones split K through
-  // a workspace, pso_gemm_ws): the register-pipelined 8-wave 128 x 128 tiles (tools/small_m_bench.py: 2048 x 1280 x
-  // 1280 + LoRA 404 vs 319 TF/s for 64 x 64); variant 49 keeps 64 x 64 there
-  if (gv_raw != 49 && !g.conv.mode && !bn64_only && (g.N % 128) == 0 && tiles(64, 160) <= 256 &&
+  // a workspace, pso_gemm_ws): variant 49 takes the register-pipelined 8-wave 128 x 128 tiles. They win in isolation
+  // (tools/small_m_bench.py: 2048 x 1280 x 1280 + LoRA 404 vs 319 TF/s) but lose inside the bs = 1 step
+  // (tools/shape_prof.py, one box: 252-256 vs 277 TF/s), so 64 x 64 stays the default there
+  if (gv_raw == 49 && !g.conv.mode && !bn64_only && (g.N % 128) == 0 && tiles(64, 160) <= 256 &&
       tiles(128, 128) >= 128 && tiles(128, 160) < 256)
     return launch<128, 128, 2, 4, 2, true>(g, st);
   if (n160 && tiles(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
@@ -1491,7 +1492,7 @@ int pso_gemm_ws(int M, int N, const void* a1, long lda1, int K1, const void* b1,
   const SplitPlan sp = gemm_split_plan(M, N, K1, a2 ? K2 : 0, a2 != nullptr, true);
   const bool ok = ws && (((uintptr_t)ws) & 15) == 0 && sp.ks >= 2 && ws_bytes >= (size_t)sp.ks * M * N * sizeof(float) &&
                   (ldo % 4) == 0 && (out_dtype == PSO_F32 ? al16(out) : al8(out)) && (g.tail_group_n % sp.bn) == 0 &&
-                  g_gemm_variant == 0;
+                  gemm_auto_variant(g_gemm_variant) == 0;
   g.ws = ok ? (float*)ws : nullptr;
   return run_gemm(g, (hipStream_t)stream);
 }

@@ -53,8 +53,26 @@ def geglu_bwd(dev, variants):
         print(line, flush=True)
 
 
+def skinny(dev):
+    """The rank-r LoRA products (N = r): us per launch back to back, for the skinny kernel form in PSO_SKINNY_VARIANT
+    (read once per process)."""
+    print(f"skinny (PSO_SKINNY_VARIANT={os.environ.get('PSO_SKINNY_VARIANT', '0')})   us/launch   GB/s of A")
+    for M, N, Kd in [(2048, 32, 1280), (2048, 96, 1280), (4096, 32, 1280), (8192, 32, 640), (2048, 32, 5120),
+                     (8192, 32, 1280), (32768, 32, 640)]:
+        a = torch.randn(M, Kd, device=dev).bfloat16()
+        w = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).bfloat16()
+        out = K.gemm(a, w)
+        ref = a.float() @ w.float().t()
+        err = ((out.float() - ref).norm() / ref.norm()).item()
+        us = 1e3 * t_ms(lambda: K.gemm(a, w), it=200)
+        print(f"{M}x{N}x{Kd}".ljust(20) + f"{us:9.2f} {M * Kd * 2 / us / 1e3:9.0f}  err {err:.1e}  "
+              f"{K.lib().pso_last_kernel().decode()}", flush=True)
+
+
 def main():
     dev = torch.device("cuda")
+    if os.environ.get("SKINNY"):
+        return skinny(dev)
     if os.environ.get("GEGLU_BWD"):
         variants = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0,0,31,45").split(",")]
         return geglu_bwd(dev, variants)
