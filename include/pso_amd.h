@@ -176,6 +176,13 @@ int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, 
  * restricted to j in that group's r columns (out is [I][r]).  group = 0: plain pso_gemm_tn. */
 int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                         long ldo, int group, void* stream);
+/* The GEGLU proj weight gradient straight into the natural row order: out[F2][J] (f32, accumulated) += alpha *
+ * A^T B where A [M][F2] is the interleaved pre-activation gradient (per 32 outputs [h 32 | gate 32], the layout
+ * pso_gemm_geglu_bwd writes) and row i of the product lands in row (i / 64) * 32 + i % 32 (+ F2 / 2 for the gate
+ * half).  128 | F2, J >= 128, 8 | J.  One pass over the reduction rows, no atomics.  Replaces the full-UNet
+ * `ff.net.0.proj` weight gradient of torch autograd under `T:857` (C3 / C4 only). */
+int pso_gemm_tn_geglu(int M, int F2, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                      long ldo, void* stream);
 /* Batched rank-r TN products (the LoRA weight gradients of one gradient unit, deferred to the unit's end and issued
  * as ONE launch per rank / orientation instead of one launch each; same arithmetic as pso_gemm_tn).  Problem i:
  *   out_jc = 0 (dB = s dY^T u):  out[c][j]  += alpha * sum_m x[m][c] * u[m][(c / group_c) * R + j]   (out [C][R])

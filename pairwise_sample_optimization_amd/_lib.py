@@ -71,6 +71,7 @@ SIGNATURES = {
     "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_gemm_tn_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
+    "pso_gemm_tn_geglu": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_gemm_tn_ws_bytes": (csz, [ci, ci, ci]),
     "pso_gemm_tn_ws": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp, csz, vp]),
     "pso_gemm_tn_rank_batch": (ci, [ci, ci, ci, vp, vp]),

@@ -846,21 +846,23 @@ __global__ void gemm_splitk_reduce_kernel(GemmArgs g, int ks) {
 // caller-owned fp32 workspace (deterministic).  The partials cost 8 M N bytes per split against 2 M N K / ks flop,
 // so only K >= 2048 qualifies.  Returns ks (0: no split) and the tile.
 struct SplitPlan { int ks, bm, bn; };
+static int g_gemm_variant = 0;
 static SplitPlan gemm_split_plan(int M, int N, int K1, int K2, bool has_tail, bool dense) {
   SplitPlan p{0, 0, 0};
   if (!dense || M <= 0 || N <= 0 || (N % 4) != 0) return p;
   const int bm = 128, bn = (N % 160) == 0 ? 160 : 128;
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nt_all = (K1 + 63) / 64 + (has_tail ? (K2 + 63) / 64 : 0);
-  if (tiles > 128 || nt_all < 32) return p;
+  // variant 51: splits of >= 8 K-tiles (the short-K M = 2048 products: 2048 x 1280 x 1280 + LoRA in two)
+  const int min_kt = g_gemm_variant == 51 ? 8 : 16;
+  if (tiles > 128 || nt_all < 2 * min_kt) return p;
   int ks = (int)((512 + tiles - 1) / tiles);
-  if (ks > nt_all / 16) ks = nt_all / 16;
+  if (ks > nt_all / min_kt) ks = nt_all / min_kt;
   if (ks < 2) return p;
   p.ks = ks; p.bm = bm; p.bn = bn;
   return p;
 }
 
-static int g_gemm_variant = 0;
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
 
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
@@ -869,9 +871,9 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
-// the variants 37-50 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// the variants 37-51 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
 // 256 x 160 8-phase tiles off / forced; ...); any other non-zero variant forces one tile shape
-static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 50) ? 0 : gv_raw; }
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 51) ? 0 : gv_raw; }
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
@@ -1201,7 +1203,7 @@ __device__ __forceinline__ s16x4 tn_tr_asm(unsigned img_base, int r0, int col0, 
 __global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J, const bf16_t* __restrict__ A,
                                                             long lda, const bf16_t* __restrict__ B, long ldb,
                                                             float alpha, float* __restrict__ out, long ldo,
-                                                            int steps, float* __restrict__ part) {
+                                                            int steps, float* __restrict__ part, int geglu_f = 0) {
   __shared__ __attribute__((aligned(16))) bf16_t sT[2][4][64 * 64];  // [stage][A0 A1 B0 B1], 64 KB
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1283,11 +1285,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn128_kernel(int M, int I, int J,
   for (int a = 0; a < 4; ++a) {
     const int i = i0 + wi * 64 + a * 16 + c;
     if (i >= I) continue;
+    // geglu_f > 0: A's columns are the GEGLU interleave (per 32 outputs [h 32 | gate 32]); row i of the product goes
+    // to row (i / 64) * 32 + i % 32 of the natural [h | gate] order, plus geglu_f for the gate half
+    const int io = geglu_f > 0 ? ((i >> 6) << 5) + (i & 31) + ((i & 32) ? geglu_f : 0) : i;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int j = j0 + wj * 64 + b * 16 + 4 * g;
       if (j >= J) continue;  // J % 8 == 0: a lane's 4 columns are all in or all out
-      float* o = out + (long)i * ldo + j;
+      float* o = out + (long)io * ldo + j;
       if (part) {  // this slice's partial product, stored (added into out by tn_reduce_slices_kernel)
         *reinterpret_cast<float4*>(part + ((long)blockIdx.y * I + i) * J + j) =
             make_float4(acc[a][b][0] * alpha, acc[a][b][1] * alpha, acc[a][b][2] * alpha, acc[a][b][3] * alpha);
@@ -1688,6 +1693,22 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   gemm_tn_kernel<<<dim3(tiles, ks), 256, 0, (hipStream_t)stream>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B,
                                                                    ldb, alpha, out, ldo, nullptr);
   return pso_check_launch("pso_gemm_tn");
+}
+
+int pso_gemm_tn_geglu(int M, int F2, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                      long ldo, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && F2 > 0 && (F2 % 128) == 0 && J >= 128 && (J % 8) == 0 && A && B && out,
+                "pso_gemm_tn_geglu: need 128 | F2 (F2=%d), J >= 128, 8 | J (J=%d)", F2, J);
+  PSO_ARG_CHECK(al16(A) && al16(B) && (lda % 8) == 0 && (ldb % 8) == 0, "pso_gemm_tn_geglu: 16-B aligned rows");
+  PSO_ARG_CHECK((long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30), "pso_gemm_tn_geglu: operand too large");
+  if (M == 0) return PSO_OK;
+  // one pass over the reduction rows (no split: += straight into the natural-order gradient, deterministic)
+  const int t128 = (F2 / 128) * ((J + 127) / 128);
+  pso_note_kernel("gemm_tn128_kernel");
+  gemm_tn128_kernel<<<dim3(t128, 1), 256, 0, (hipStream_t)stream>>>(M, F2, J, (const bf16_t*)A, lda, (const bf16_t*)B,
+                                                                     ldb, alpha, out, ldo, (M + 63) / 64, nullptr,
+                                                                     F2 / 2);
+  return pso_check_launch("pso_gemm_tn_geglu");
 }
 
 }  // extern "C"

@@ -289,6 +289,20 @@ def gemm_tn(a, b, out, alpha=1.0, group=0, split_ws=True):
     return out
 
 
+def gemm_tn_geglu(df, x, out, alpha=1.0):
+    """out[F2, J] (f32, accumulated) += alpha * df^T @ x with df [M, F2] in the GEGLU interleave (geglu_interleave_index)
+    and out in the natural [h | gate] row order: the full-UNet ff.net.0.proj weight gradient without a transient
+    interleaved matrix (pso_gemm_tn_geglu)."""
+    M, F2 = df.shape
+    J = x.shape[1]
+    assert x.shape[0] == M and out.shape == (F2, J) and out.dtype == torch.float32
+    e0 = _prof_begin()
+    check(lib().pso_gemm_tn_geglu(M, F2, J, ptr(df), _row_stride(df), ptr(x), _row_stride(x), float(alpha), ptr(out),
+                                  _row_stride(out), stream_ptr()), "pso_gemm_tn_geglu")
+    _prof_end(e0, 2.0 * M * F2 * J, 2.0 * M * (F2 + J) + 8.0 * F2 * J, ("gemm_tn", M, F2, J, 0))
+    return out
+
+
 def _tn_rank_form(a, b, group):
     """(key, x, u, R, group_c) of a TN product gemm_tn(a, b, ...) that the rank-r streaming kernel takes, else None:
     x the >= 128-wide side, u the rank-R side, key = (R, out_jc)."""

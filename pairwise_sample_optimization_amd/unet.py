@@ -239,6 +239,7 @@ class FullGradState:
 
 
 _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
+_GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"  # ff.proj dW straight into the natural rows (pso_gemm_tn_geglu)
 
 
 def _lin_dw(fg, lin, dy, x, rt=None):
@@ -583,14 +584,18 @@ class BasicTransformerBlock(nn.Module):
             n3 = sv["n3"]
 
             def ff_proj_dw():
+                # df's columns are in the GEGLU interleave (per 32 outputs [h 32 | gate 32]): the weight gradient
+                # lands in the natural row order from the TN epilogue, the bias sum through a strided view
                 F2 = df.shape[1]
-                idx = K.geglu_interleave_index(F2 // 2, df.device)
-                tmp = torch.zeros((F2, C), device=df.device, dtype=torch.float32)
-                K.gemm_tn(df, n3, tmp)
-                fg.g(self.ff.proj.weight).index_add_(0, idx, tmp)
+                if _GEGLU_TN:
+                    K.gemm_tn_geglu(df, n3, fg.g(self.ff.proj.weight))
+                else:  # benchmark knob PSO_GEGLU_TN=0: the transient interleaved matrix + index_add (round 3)
+                    tmp = torch.zeros((F2, C), device=df.device, dtype=torch.float32)
+                    K.gemm_tn(df, n3, tmp)
+                    fg.g(self.ff.proj.weight).index_add_(0, K.geglu_interleave_index(F2 // 2, df.device), tmp)
                 tb = torch.zeros((1, F2), device=df.device, dtype=torch.float32)
                 K.colsum_acc(df, tb)
-                fg.g(self.ff.proj.bias).index_add_(0, idx, tb[0])
+                fg.g(self.ff.proj.bias).view(2, F2 // 64, 32).add_(tb.view(F2 // 64, 2, 32).transpose(0, 1))
             rt.side.launch(ff_proj_dw, df, n3)
         dn3 = K.gemm(df, self.ff.wt_int)
         if fg is not None:

@@ -156,6 +156,27 @@ def test_gemm_tn_vs_fp32(cuda, M, I, J, split_ws):
         assert torch.equal(o1, o2)
 
 
+@pytest.mark.parametrize("M,F,J", [(6144, 5120, 1280), (1000, 2560, 640), (77, 128, 264)])
+def test_gemm_tn_geglu_natural_rows(cuda, M, F, J):
+    """The GEGLU proj weight gradient from the interleaved pre-activation gradient (per 32 outputs [h 32 | gate 32])
+    straight into the natural [h | gate] row order: equals the interleaved product scattered by
+    geglu_interleave_index (the transient-matrix + index_add form it replaces) bit for bit, and fp32 to 1e-5."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    df = torch.randn(M, 2 * F, device=cuda).bfloat16()
+    x = torch.randn(M, J + 8, device=cuda).bfloat16()[:, :J]
+    base = torch.randn(2 * F, J, device=cuda)
+    idx = K_.geglu_interleave_index(F, cuda)
+    tmp = torch.zeros(2 * F, J, device=cuda)
+    K_.gemm_tn(df, x, tmp, split_ws=False)
+    want = base.clone().index_add_(0, idx, tmp)
+    out = base.clone()
+    K_.gemm_tn_geglu(df, x, out)
+    ref = base.clone().index_add_(0, idx, df.float().t() @ x.float())
+    assert _rel(out, ref) < 1e-5
+    if K_.lib().pso_gemm_tn_ws_bytes(M, 2 * F, J) == 0 and 2 * F >= 128 and J >= 128:  # same tiles, one pass
+        assert torch.equal(out, want)
+
+
 @pytest.mark.parametrize("M,C,G", [(8192, 1280, 3), (1000, 640, 3), (616, 1280, 2)])
 def test_gemm_grouped_skinny(cuda, M, C, G):
     """Block-diagonal v = dy sB of the fused q/k/v (G = 3) and cross k/v (G = 2) adapters."""
