@@ -278,6 +278,17 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
                int ks, int stride, int pad, const void* weight, int Cout, const void* a2, long lda2, int K2,
                const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
                const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate, void* stream);
+/* Deterministic split-K form of pso_conv2d for small outputs with a long reduction (the bs = 1 / GPU backward's
+ * input-gradient convolutions at 2 images: 2048 x 1280 x 11520): same arguments plus a caller-owned fp32 workspace of
+ * pso_conv2d_ws_bytes(B, Ho, Wo, Cout, ks*ks*(C1+C2), K2) bytes (0: no split applies, pso_conv2d is used); every
+ * K-split stores its partial product and they are added in split order with the epilogue (bias, row bias,
+ * residual) applied once.  No atomics. */
+size_t pso_conv2d_ws_bytes(int B, int Ho, int Wo, int Cout, int K1, int K2);
+int pso_conv2d_ws(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+                  int ks, int stride, int pad, const void* weight, int Cout, const void* a2, long lda2, int K2,
+                  const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+                  const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate, void* ws,
+                  size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------------
  * GroupNorm (+ fused SiLU) on NHWC bf16, fp32 statistics.  stats [B][G][2] = (mean, rstd).

@@ -85,6 +85,9 @@ SIGNATURES = {
                           vp, cl, vp, cl, ci, vp]),
     "pso_conv2d": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
                         cl, vp, cl, vp, cl, ci, ci, vp]),
+    "pso_conv2d_ws_bytes": (csz, [ci, ci, ci, ci, ci, ci]),
+    "pso_conv2d_ws": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, ci, vp, ci, vp, cl, ci, vp, cl, cf, vp, vp,
+                           cl, vp, cl, vp, cl, ci, ci, vp, csz, vp]),
     "pso_group_norm_ws_bytes": (csz, [ci, ci, ci]),
     "pso_group_norm_fwd": (ci, [ci, ci, ci, ci, cf, vp, vp, vp, ci, vp, vp, vp, csz, vp]),
     "pso_group_norm_bwd": (ci, [ci, ci, ci, ci, vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, ci, vp, csz, vp]),

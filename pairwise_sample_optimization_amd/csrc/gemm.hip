@@ -871,9 +871,16 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
-// the variants 37-51 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// the variants 37-52 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
 // 256 x 160 8-phase tiles off / forced; ...); any other non-zero variant forces one tile shape
-static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 51) ? 0 : gv_raw; }
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 52) ? 0 : gv_raw; }
+// the workspace split-K forms (pso_gemm_ws / pso_conv2d_ws) under the benchmark knobs: off where a variant forces a
+// tile (38 / 39 / 44: the 8-phase 256 x 160 / 256 x 320 / conv tiles, the tests that pin them), where a raster group
+// is forced, and under variant 52 (the conv split off)
+static bool gemm_ws_allowed() {
+  const int v = g_gemm_variant;
+  return g_gemm_group == 0 && gemm_auto_variant(v) == 0 && v != 38 && v != 39 && v != 44 && v != 52;
+}
 
 static int run_gemm(GemmArgs& g, hipStream_t st) {
   const int gv_raw = g_gemm_variant;
@@ -902,7 +909,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   }
   // deterministic split-K through the caller's workspace (pso_gemm_ws): small M x N, long K
   if (g.ws) {
-    const SplitPlan sp = gemm_split_plan(g.M, g.N, g.K1, g.K2, g.a2 != nullptr, !g.conv.mode);
+    const SplitPlan sp = gemm_split_plan(g.M, g.N, g.K1, g.K2, g.a2 != nullptr, true);  // entries checked the form
     if (sp.ks >= 2) {
       if (sp.bn == 160) launch<128, 160, 2, 2, 2>(g, st, sp.ks);
       else launch<128, 128, 2, 4, 2>(g, st, sp.ks);
@@ -1497,7 +1504,7 @@ int pso_gemm_ws(int M, int N, const void* a1, long lda1, int K1, const void* b1,
   const SplitPlan sp = gemm_split_plan(M, N, K1, a2 ? K2 : 0, a2 != nullptr, true);
   const bool ok = ws && (((uintptr_t)ws) & 15) == 0 && sp.ks >= 2 && ws_bytes >= (size_t)sp.ks * M * N * sizeof(float) &&
                   (ldo % 4) == 0 && (out_dtype == PSO_F32 ? al16(out) : al8(out)) && (g.tail_group_n % sp.bn) == 0 &&
-                  gemm_auto_variant(g_gemm_variant) == 0;
+                  gemm_ws_allowed();
   g.ws = ok ? (float*)ws : nullptr;
   return run_gemm(g, (hipStream_t)stream);
 }
@@ -1549,6 +1556,52 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = Ho * Wo;
   g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  return run_gemm(g, (hipStream_t)stream);
+}
+
+size_t pso_conv2d_ws_bytes(int B, int Ho, int Wo, int Cout, int K1, int K2) {
+  const long M = (long)B * Ho * Wo;
+  if (M <= 0 || M > 0x7fffffffL) return 0;
+  const SplitPlan sp = gemm_split_plan((int)M, Cout, K1, K2, K2 > 0, true);
+  return sp.ks >= 2 ? (size_t)sp.ks * M * Cout * sizeof(float) : 0;
+}
+
+int pso_conv2d_ws(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
+                  int ks, int stride, int pad, const void* weight, int Cout, const void* a2, long lda2, int K2,
+                  const void* b2, long ldb2, float alpha, const void* bias, const void* rowbias, long ld_rowbias,
+                  const void* resid, long ldr, void* out, long ldo, int out_dtype, int accumulate, void* ws,
+                  size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(mode == PSO_CONV_NORMAL || mode == PSO_CONV_UP2 || mode == PSO_CONV_T2, "pso_conv2d_ws: bad mode");
+  PSO_ARG_CHECK(src1 && weight && out, "pso_conv2d_ws: null operand");
+  PSO_ARG_CHECK((C1 % 64) == 0 && (C2 % 64) == 0 && (C2 == 0 || src2),
+                "pso_conv2d_ws: channel sources must be multiples of 64 (C1=%d C2=%d)", C1, C2);
+  PSO_ARG_CHECK(al16(src1) && (!src2 || al16(src2)) && al16(weight), "pso_conv2d_ws: alignment");
+  PSO_ARG_CHECK(ks == 1 || ks == 3, "pso_conv2d_ws: ks must be 1 or 3");
+  PSO_ARG_CHECK(mode != PSO_CONV_UP2 || (Ho == 2 * H && Wo == 2 * W && stride == 1), "pso_conv2d_ws: UP2 geometry");
+  PSO_ARG_CHECK(!a2 || ((K2 % 8) == 0 && b2 && al16(a2) && al16(b2)), "pso_conv2d_ws: bad second operand");
+  PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_conv2d_ws: accumulate needs f32 output");
+  GemmArgs g{};
+  const int Ct = C1 + C2;
+  g.a1 = (const bf16_t*)src1; g.lda1 = 0; g.K1 = ks * ks * Ct;
+  g.b1 = (const bf16_t*)weight; g.ldb1 = g.K1;
+  g.a2 = (const bf16_t*)a2; g.lda2 = lda2; g.K2 = a2 ? K2 : 0;
+  g.b2 = (const bf16_t*)b2; g.ldb2 = ldb2;
+  g.M = B * Ho * Wo; g.N = Cout;
+  g.tail_m = g.M;
+  g.conv.mode = mode; g.conv.src2 = (const bf16_t*)src2; g.conv.C1 = C1; g.conv.C2 = C2;
+  g.conv.H = H; g.conv.W = W; g.conv.Ho = Ho; g.conv.Wo = Wo; g.conv.ks = ks; g.conv.stride = stride; g.conv.pad = pad;
+  g.alpha = alpha;
+  g.bias = (const bf16_t*)bias;
+  g.rowbias = (const bf16_t*)rowbias; g.ld_rowbias = ld_rowbias; g.rows_per_group = Ho * Wo;
+  g.resid = (const bf16_t*)resid; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.accumulate = accumulate;
+  // the workspace form applies when the plan splits and the workspace holds every split; else the plain conv
+  const SplitPlan sp = gemm_split_plan(g.M, g.N, g.K1, g.K2, g.a2 != nullptr, true);
+  const bool ok = ws && (((uintptr_t)ws) & 15) == 0 && sp.ks >= 2 && ws_bytes >= (size_t)sp.ks * g.M * g.N * sizeof(float) &&
+                  (ldo % 4) == 0 && (out_dtype == PSO_F32 ? al16(out) : al8(out)) && (g.N % 4) == 0 &&
+                  (!resid || ((ldr % 4) == 0 && al8(resid))) && (!rowbias || (ld_rowbias % 4) == 0) &&
+                  gemm_ws_allowed();
+  g.ws = ok ? (float*)ws : nullptr;
   return run_gemm(g, (hipStream_t)stream);
 }
 

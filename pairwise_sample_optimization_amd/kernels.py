@@ -385,13 +385,21 @@ def conv2d(x, weight, *, x2=None, mode=CONV_NORMAL, stride=1, pad=None, out_hw=N
     K2 = a2.shape[1] if a2 is not None else 0
     o2 = out.view(B * Ho * Wo, -1) if out.is_contiguous() else None
     ldo = Cout if o2 is None else o2.stride(0)
+    key = ("conv", B, Ho, Wo, Cout, ks * ks * Ct, K2)
+    wsb = _GEMM_WS.get(key)
+    if wsb is None:
+        wsb = _GEMM_WS[key] = int(lib().pso_conv2d_ws_bytes(B, Ho, Wo, Cout, ks * ks * Ct, K2))
+    args = (mode, B, ptr(x), C1, ptr(x2), C2, H, W, Ho, Wo, ks, stride, pad, ptr(weight), Cout,
+            ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
+            ptr(w2), _row_stride(w2) if w2 is not None else 0, float(alpha), ptr(bias),
+            ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
+            ptr(resid), Cout if resid is not None else 0, ptr(out), ldo, dtype_code(out), int(accumulate))
     e0 = _prof_begin()
-    check(lib().pso_conv2d(mode, B, ptr(x), C1, ptr(x2), C2, H, W, Ho, Wo, ks, stride, pad, ptr(weight), Cout,
-                           ptr(a2), _row_stride(a2) if a2 is not None else 0, K2,
-                           ptr(w2), _row_stride(w2) if w2 is not None else 0, float(alpha), ptr(bias),
-                           ptr(rowbias), rowbias.stride(0) if rowbias is not None else 0,
-                           ptr(resid), Cout if resid is not None else 0, ptr(out), ldo, dtype_code(out),
-                           int(accumulate), stream_ptr()), "pso_conv2d")
+    if wsb:  # small output, long reduction (bs = 1 backward): deterministic split-K through a workspace
+        ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
+        check(lib().pso_conv2d_ws(*args, ptr(ws), wsb, stream_ptr()), "pso_conv2d_ws")
+    else:
+        check(lib().pso_conv2d(*args, stream_ptr()), "pso_conv2d")
     _prof_end(e0, 2.0 * B * Ho * Wo * Cout * (ks * ks * (C1 + C2) + K2),
               2.0 * (B * H * W * (C1 + C2) + Cout * ks * ks * (C1 + C2) + B * Ho * Wo * K2 + Cout * K2)
               + out.element_size() * B * Ho * Wo * Cout, ("conv", mode, B, H, W, C1, C2, Cout, ks, stride, K2))

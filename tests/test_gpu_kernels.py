@@ -95,6 +95,36 @@ def test_conv_normal(cuda, B, C1, C2, H, Cout, ks, stride):
     assert _rel(_nchw(out), ref) < 1e-5
 
 
+@pytest.mark.parametrize("C1,C2,Cout", [(1280, 0, 1280), (1280, 640, 640)])
+def test_conv_splitk_workspace(cuda, C1, C2, Cout):
+    """The bs = 1 backward's input-gradient convolutions (2 images at 32 x 32, K = 9 * 1920 / 11520): few output
+    tiles, long reduction -> pso_conv2d_ws (K-splits stored, added in split order, bias / time-embedding / residual
+    applied once).  fp32 reference; bit-identical on repeat; the unsplit kernel (variant 52) within bf16 rounding."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    B, H, Ct = 2, 32, C1 + C2
+    assert K_.lib().pso_conv2d_ws_bytes(B, H, H, Cout, 9 * Ct, 0) > 0
+    x = torch.randn(B, Ct, H, H, device=cuda).bfloat16()
+    w = (torch.randn(Cout, Ct, 3, 3, device=cuda) / (3 * Ct ** 0.5)).bfloat16()
+    bias = torch.randn(Cout, device=cuda).bfloat16()
+    temb = torch.randn(B, Cout, device=cuda).bfloat16()
+    res = torch.randn(B, H, H, Cout, device=cuda).bfloat16()
+    ref = F.conv2d(x.float(), w.float(), bias.float(), padding=1) + temb.float()[:, :, None, None]
+    xh = _nhwc(x)
+    x1, x2 = xh[..., :C1].contiguous(), (xh[..., C1:].contiguous() if C2 else None)
+    o32 = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, out_dtype=torch.float32)
+    assert _rel(_nchw(o32), ref) < 1e-5
+    ob = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
+    ob2 = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
+    assert torch.equal(ob, ob2)
+    assert _rel(_nchw(ob), ref + _nchw(res.float())) < 4e-3
+    K_.lib().pso_gemm_set_variant(52)
+    try:
+        on = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
+    finally:
+        K_.lib().pso_gemm_set_variant(0)
+    assert _rel(ob, on) < 4e-3
+
+
 def test_conv_up2(cuda):
     from pairwise_sample_optimization_amd import kernels as K_
     x = torch.randn(2, 128, 8, 8, device=cuda).bfloat16()
