@@ -239,6 +239,10 @@ class FullGradState:
 
 
 _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
+# fp8 forward (config 5): which LayerNorm-fed projections take the e4m3 kernel (diagnostics: tools/diag_fp8_grads.py)
+# "tail": the LoRA up-projection as an e4m3 K-tail; "qkv" (the self-attention q/k/v) is off by default, see
+# enable_fp8_forward
+FP8_KINDS = {"q2", "ff", "tail"}
 _GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"  # ff.proj dW straight into the natural rows (pso_gemm_tn_geglu)
 
 
@@ -492,18 +496,23 @@ class BasicTransformerBlock(nn.Module):
         n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
         f8 = rt.fp8  # fp8 forward (config 5): the LayerNorm-fed projections on e4m3 MFMA where the shapes allow
         # (the fp8 LoRA tail reads 16-B rows of the rank-r operands: r % 16 == 0)
-        ok8 = lambda n_out, k_in: (f8 is not None and n_out % 256 == 0 and k_in % 128 == 0 and
-                                   (not lo or rt.r % 16 == 0))
+        ok8 = lambda n_out, k_in, kind: (f8 is not None and kind in FP8_KINDS and n_out % 256 == 0 and
+                                         k_in % 128 == 0 and (not lo or rt.r % 16 == 0))
         ver = rt.lora.version if lo else 0
         if lo:
             u_qkv = K.gemm(pol(n1), L.A_qkv)                                # [Mp, 3r]
-            if ok8(3 * C, C):
+            if ok8(3 * C, C, "qkv") and "tail" not in FP8_KINDS:  # diagnostics: the LoRA term in bf16
+                qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv))
+                for j in range(3):
+                    sl = qkv[:Mp, j * C:(j + 1) * C]
+                    sl.copy_(K.gemm(u_qkv[:, j * r:(j + 1) * r], L.sB_qkv[j * C:(j + 1) * C], resid=sl))
+            elif ok8(3 * C, C, "qkv"):
                 qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv),
                                  a2=K.quant_rows_fp8(u_qkv), w2=f8((id(self), "sB_qkv"), L.sB_qkv, ver),
                                  tail_group_n=C, tail_rows=tr)
             else:
                 qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
-        elif ok8(3 * C, C):
+        elif ok8(3 * C, C, "qkv"):
             qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv))
         else:
             qkv = K.gemm(n1, a1m.w_qkv)
@@ -522,12 +531,15 @@ class BasicTransformerBlock(nn.Module):
         Se = enc.shape[0] // B
         if lo:
             u_q2 = K.gemm(pol(n2), L.A_q2)
-            if ok8(C, C):
+            if ok8(C, C, "q2") and "tail" not in FP8_KINDS:  # diagnostics: the LoRA term in bf16
+                q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight))
+                q2[:Mp].copy_(K.gemm(u_q2, L.sB_q2, resid=q2[:Mp]))
+            elif ok8(C, C, "q2"):
                 q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight),
                                 a2=K.quant_rows_fp8(u_q2), w2=f8((id(self), "sB_q2"), L.sB_q2, ver), tail_rows=tr)
             else:
                 q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
-        elif ok8(C, C):
+        elif ok8(C, C, "q2"):
             q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight))
         else:
             q2 = K.gemm(n2, a2m.to_q.weight)
@@ -548,7 +560,7 @@ class BasicTransformerBlock(nn.Module):
         n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
         ff = self.ff
         f = torch.empty((Mp, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
-        if ok8(ff.w_int.shape[0], C):
+        if ok8(ff.w_int.shape[0], C, "ff"):
             gg = K.gemm_fp8(K.quant_rows_fp8(n3), f8((id(self), "ff"), ff.w_int), bias=ff.b_int, geglu=True, out_pre=f,
                             pre_rows=Mp)
         else:
@@ -1185,12 +1197,14 @@ class UNet2DConditionModel(nn.Module):
 
     # ---------------- fp8 forward (BASELINE config 5) ----------------
     def enable_fp8_forward(self, on=True):
-        """Run the LayerNorm-fed projections of every transformer block -- the fused self-attention q/k/v, the
-        cross-attention q and the GEGLU ff.net.0.proj, 2/3 of a block's projection FLOPs -- on fp8 e4m3 MFMA
-        (pso_gemm_fp8: per-token activation scales, per-output-channel weight scales, the LoRA up-projection as an fp8
-        K-tail); everything else, and the whole backward, stays bf16 (BASELINE config 5: "fp8 MFMA UNet fwd + bf16
-        bwd").  Shapes the fp8 kernel does not take (N % 256 or K % 128 != 0: the 640-wide q/k/v of the 64^2 level)
-        stay bf16.  LoRA training only (the base weights are quantised once and cached)."""
+        """Run the LayerNorm-fed projections of every transformer block named in FP8_KINDS -- the cross-attention q
+        and the GEGLU ff.net.0.proj by default -- on fp8 e4m3 MFMA (pso_gemm_fp8: per-token activation scales,
+        per-output-channel weight scales, the LoRA up-projection as an fp8 K-tail); everything else, and the whole
+        backward, stays bf16 (BASELINE config 5: "fp8 MFMA UNet fwd + bf16 bwd").  The fused self-attention q/k/v
+        ("qkv") is kept out by default: e4m3 q and k move the softmax logits, and on the C5 micro-step it alone
+        carries a 7.5e-2 LoRA-gradient error (cross q 5.6e-3, GEGLU proj 3.5e-2; tools/diag_fp8_grads.py) while running
+        slower than bf16.  Shapes the fp8 kernel does not take (N % 256 or K % 128 != 0) stay bf16.  LoRA training
+        only (the base weights are quantised once and cached)."""
         if on and self.full is not None:
             raise ValueError("fp8 forward: LoRA training only (the full-UNet mode updates the base weights)")
         self.fp8 = bool(on)

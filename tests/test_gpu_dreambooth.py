@@ -76,11 +76,11 @@ def test_dreambooth_micro_step_vs_fp32_reference(cuda, loss_type, B):
 def test_dreambooth_micro_step_fp8_at_1024(cuda):
     """BASELINE config 5 at its per-GPU workload: the DreamBooth PSO micro-step (DB:1720-1964, recipe
     scripts/pso_dog.sh: pso_db, beta 5, rank 16, 1 instance + 1 negative image) at 1024^2 with the full SDXL UNet and
-    VAE encoder, with the fp8 forward on (enable_fp8_forward: e4m3 q/k/v, cross q, GEGLU proj; bf16 backward), against
+    VAE encoder, with the fp8 forward on (enable_fp8_forward: e4m3 cross q and GEGLU proj; bf16 backward), against
     the fp32 oracle micro-step on the same latents / noise / timesteps.  The bf16 forward runs beside it on the same
-    inputs so the fp8 cost is visible.  Stated fp8 tolerance: loss rel <= 5e-2, LoRA grad rel <= 0.25 (e4m3 has 3
-    mantissa bits; the bf16 forward's bars are 2e-2 / 1e-1; the fp8 UNet forward test at sdxl64 measured eps 2e-2 and
-    grads 0.14)."""
+    inputs so the fp8 cost is visible.  Stated fp8 tolerance: loss rel <= 5e-3, LoRA grad rel <= 5e-2 (e4m3 has 3
+    mantissa bits; the bf16 forward's bars are 2e-2 / 1e-1; round 3 also ran the self-attention q/k/v in e4m3: grad
+    rel 8.6e-2, 7.5e-2 of it from q/k/v alone, tools/diag_fp8_grads.py)."""
     from oracle import sdxl_ref
     from pairwise_sample_optimization_amd import kernels as K
     from pairwise_sample_optimization_amd.dreambooth import DreamBoothPSOTrainer
@@ -144,4 +144,4 @@ def test_dreambooth_micro_step_fp8_at_1024(cuda):
           f"{grel[False]:.3e} fp8 {grel[True]:.3e}")
     assert den > 0
     assert rel[False] < 2e-2 and grel[False] < 1e-1
-    assert rel[True] < 5e-2 and grel[True] < 0.25
+    assert rel[True] < 5e-3 and grel[True] < 5e-2

@@ -105,11 +105,12 @@ def test_gemm_fp8_geglu(cuda, M, Fd, K, pre_rows):
 
 @pytest.mark.parametrize("which", ["sdxl32", "sdxl64"])
 def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which):
-    """The whole SDXL UNet with enable_fp8_forward() (fp8 q/k/v, cross q, GEGLU proj; bf16 elsewhere; bf16 backward)
+    """The whole SDXL UNet with enable_fp8_forward() (fp8 cross q and GEGLU proj; bf16 elsewhere; bf16 backward)
     against the fp32 oracle: eps and every LoRA gradient.  Bars: the bf16 path's (3e-2 / 5e-2) widened by the e4m3
     operand rounding (3 mantissa bits: ~2^-5 relative per operand, averaged over K).  The gradients move more than eps
-    (measured 0.117 vs 0.03 for the bf16 forward at sdxl32): the backward runs on the fp8 forward's q/k/v and GEGLU
-    pre-activations, so their rounding enters every attention / GEGLU backward product."""
+    (round 4: eps 1.1e-2, grads 5.3e-2 / 5.8e-2 at sdxl32 / 64; round 3, with the self-attention q/k/v in e4m3 too:
+    0.117 / 0.14): the backward runs on the fp8 forward's cross q and GEGLU pre-activations, so their rounding enters
+    the attention / GEGLU backward products."""
     from test_gpu_unet import _oracle, _setup
     from pairwise_sample_optimization_amd.unet import UNetConfig
     cfg = UNetConfig.sdxl(32 if which == "sdxl32" else 64)
@@ -132,5 +133,5 @@ def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which):
     den = sum((v.grad ** 2).sum().item() for v in leaf.values())
     g_rel = (num / den) ** 0.5
     print(f"{which}: eps rel err bf16 {e_bf:.3e} fp8 {e_f8:.3e}; lora grad rel err (fp8 fwd, bf16 bwd) {g_rel:.3e}")
-    assert e_f8 < 6e-2 and g_rel < 2e-1
+    assert e_f8 < 3e-2 and g_rel < 1e-1
     unet.enable_fp8_forward(False)
