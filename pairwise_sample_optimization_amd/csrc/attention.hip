@@ -647,6 +647,16 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
       vf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(V + (long)kr * a.ldv + ds * 32 + 8 * g));
     }
   }
+  // PF: byte offset (inside a 64 x 64 transposed-read image) of this lane's ds_read_b64_tr_b16 for d-block dt at query
+  // rows 0..15; the query row block (32 qk + 16 h) adds (32 qk + 16 h) * 128 B and the dO image sits 16 KB after the Q
+  // image, so one base register per dt serves all 32 transposed reads of a tile through the instruction's offset field
+  unsigned troff[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int li = lane & 15;
+    const int col = dt * 16 + 4 * (li & 3);
+    troff[dt] = 2u * (unsigned)(swz_tr(4 * g + (li >> 2), col >> 3) + (col & 7));
+  }
   f32x4 dk[KJ][4], dv[KJ][4];  // [kj][dt]: lane holds d?[k = kj*16 + c][d = dt*16 + 4g + r]
 #pragma unroll
   for (int kj = 0; kj < KJ; ++kj)
@@ -670,11 +680,15 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
     const bool qpart = qbase + ATT_KT > a.Sq;
     float4 lpf[4], dpf[4];
     if constexpr (PF) {
-#pragma unroll
-      for (int qs = 0; qs < 4; ++qs) {
-        asm volatile("ds_read_b128 %0, %1" : "=v"(lpf[qs]) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sL + qs * 16 + 4 * g)));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(dpf[qs]) : "v"((unsigned)(uintptr_t)(const att_lds_void*)(sD + qs * 16 + 4 * g)));
-      }
+      const unsigned lb = (unsigned)(uintptr_t)(const att_lds_void*)(sL + 4 * g);  // sD = sL + 64 floats (256 B)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(lpf[0]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(lpf[1]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:128" : "=v"(lpf[2]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:192" : "=v"(lpf[3]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:256" : "=v"(dpf[0]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:320" : "=v"(dpf[1]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:384" : "=v"(dpf[2]) : "v"(lb));
+      asm volatile("ds_read_b128 %0, %1 offset:448" : "=v"(dpf[3]) : "v"(lb));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -705,7 +719,9 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         }
         float lq[4] = {l4.x, l4.y, l4.z, l4.w};  // LSE * log2(e), from the dQ kernel
         const f32x4 ndel = {d4.x, d4.y, d4.z, d4.w};  // -delta, from the dQ kernel
-        if (qpart) {
+        // PF: no mask -- query rows past Sq read as zeros (Q, dO and the LSE / delta resources end at row Sq - 1), so a
+        // padded row has S = 0, p = 1, dP = 0 and dS = 0, and its zero Q / dO rows add nothing to dK / dV
+        if (!PF && qpart) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (qbase + qs * 16 + 4 * g + r >= a.Sq) lq[r] = INFINITY;  // padded query rows: p = 0
@@ -732,13 +748,20 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         // the wait is tied to the 16 read registers (no scheduling barrier): only the dV / dK MFMAs wait for it, so
         // the compiler may interleave them with the next subtile's independent work
         s16x4 otr[8], qtr[8];
+        const unsigned qtb = (unsigned)(uintptr_t)(const att_lds_void*)sQt;  // sOt = sQt + 16 KB
+        auto trd = [&](auto QK_) {
+          constexpr int o = decltype(QK_)::value * 4096;  // query rows 32 qk ..
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          otr[2 * dt] = tr_read_asm(sOt, (2 * qk) * 16 + 4 * g, dt * 16, lane);
-          otr[2 * dt + 1] = tr_read_asm(sOt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane);
-          qtr[2 * dt] = tr_read_asm(sQt, (2 * qk) * 16 + 4 * g, dt * 16, lane);
-          qtr[2 * dt + 1] = tr_read_asm(sQt, (2 * qk + 1) * 16 + 4 * g, dt * 16, lane);
-        }
+          for (int dt = 0; dt < 4; ++dt) {
+            const unsigned ab = qtb + troff[dt];
+            qtr[2 * dt] = tr_read_imm<o>(ab);
+            qtr[2 * dt + 1] = tr_read_imm<o + 2048>(ab);
+            otr[2 * dt] = tr_read_imm<16384 + o>(ab);
+            otr[2 * dt + 1] = tr_read_imm<16384 + o + 2048>(ab);
+          }
+        };
+        if (qk == 0) trd(ic<0>{});
+        else trd(ic<1>{});
         lds_wait8(otr);
         lds_wait8(qtr);
 #pragma unroll
