@@ -1,1 +1,1 @@
-bash tools/gpu_steps.sh "at|300|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_layers.py -k attention" "ab|120|ATTN_VARIANTS=0,10,0,10 python tools/attn_bench.py" "atd|300|python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_determinism.py" && bash tools/ab.sh attn "0 10" 2 > gpurun_out/ab_attn_c2.log 2>&1
+SKIP_TESTS=1 bash tools/gpu_full.sh
