@@ -1,1 +1,1 @@
-SKIP_TESTS=1 bash tools/gpu_full.sh
+bash tools/gpu_steps.sh "shg|150|python tools/shape_prof.py" "shg2|150|python tools/shape_prof.py"
