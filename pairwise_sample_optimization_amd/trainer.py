@@ -21,10 +21,26 @@ from types import SimpleNamespace
 import torch
 import torch.distributed as dist
 
+import os
+
 from . import kernels as K
 from . import pso_core
 from ._lib import MODE_TURBO, MODE_DMD
 from .schedulers import EulerAncestralDiscreteScheduler, LCMScheduler, dmd_distill_timesteps
+
+# full-UNet mode: the frozen reference pass on a stream of its own (PSO_REF_STREAM=0 keeps it in line, A/B knob)
+_REF_STREAM = os.environ.get("PSO_REF_STREAM", "1") == "1"
+_REF_STREAMS = {}
+
+
+def _ref_stream():
+    """ONE reference-pass stream per device for the process (the caching allocator keeps freed blocks per stream)."""
+    dev = torch.cuda.current_device()
+    st = _REF_STREAMS.get(dev)
+    if st is None:
+        st = _REF_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return st
+
 
 BF16 = torch.bfloat16
 
@@ -500,9 +516,21 @@ class PSOTrainer:
         P = self.P * count
         u = self.unet
         if self.ref_unet is not None:  # full-UNet training: policy pass + the frozen reference UNet's pass
-            eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
-            with torch.no_grad():
-                eps_ref, _ = self.ref_unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
+            rs = _ref_stream() if _REF_STREAM and mb.unet_in.is_cuda else None
+            if rs is not None:
+                # the reference pass (different weights, same inputs, no saved state) on its own stream, beside the
+                # policy pass: two grids of the small-M (6 images) GEMMs / attention fill the chip together
+                main = torch.cuda.current_stream()
+                rs.wait_stream(main)
+                with torch.cuda.stream(rs), torch.no_grad():
+                    eps_ref, _ = self.ref_unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
+                eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
+                main.wait_stream(rs)
+                eps_ref.record_stream(main)
+            else:
+                eps_pol, rt = u.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=True)
+                with torch.no_grad():
+                    eps_ref, _ = self.ref_unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False)
         else:
             u.enable_adapters()
             # policy (LoRA on, T:775-787) and reference (adapters disabled, T:790-805) eps of the same inputs in ONE pass

@@ -295,6 +295,19 @@ def test_full_unet_micro_step_vs_fp32_reference(cuda):
     tr.auto_step = False
     mine_loss = tr.micro_step(mb).item()
     mine = {unet._unmap_key(n): fg.g(p).clone() for n, p in unet.named_parameters()}
+    # the reference pass on its own stream (default) and in line: the same loss bits, the same gradients (up to the
+    # f32-atomic order of the full-UNet bias / norm parameter sums)
+    from pairwise_sample_optimization_amd import trainer as T_
+    assert T_._REF_STREAM
+    T_._REF_STREAM = False
+    try:
+        g0 = fg.grad.clone()
+        fg.grad.zero_()
+        inline_loss = tr.micro_step(mb).item()
+        assert inline_loss == mine_loss
+        assert ((fg.grad - g0).norm() / g0.norm()).item() < 1e-5
+    finally:
+        T_._REF_STREAM = True
     sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
     leaf = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
     ocfg = dict(time_proj_dim=cfg.time_proj_dim, addition_time_embed_dim=cfg.addition_time_embed_dim)
