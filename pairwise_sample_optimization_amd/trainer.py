@@ -15,6 +15,7 @@ members of every pair ride in ONE UNet batch (image order 2p + k), policy and re
 weights, the loss kernel consumes the bf16 NHWC eps directly and emits d loss / d eps for the hand-written UNet
 backward, which accumulates LoRA grads into the flat all-reduce bucket.
 """
+import gc
 import math
 from types import SimpleNamespace
 
@@ -30,6 +31,7 @@ from .schedulers import EulerAncestralDiscreteScheduler, LCMScheduler, dmd_disti
 
 # full-UNet mode: the frozen reference pass on a stream of its own (PSO_REF_STREAM=0 keeps it in line, A/B knob)
 _REF_STREAM = os.environ.get("PSO_REF_STREAM", "1") == "1"
+_GC_PAUSE = os.environ.get("PSO_GC_PAUSE", "1") == "1"  # train_epoch: cyclic GC paused (A/B knob)
 _REF_STREAMS = {}
 
 
@@ -617,7 +619,19 @@ class PSOTrainer:
 
     def train_epoch(self, sb, generator=None):
         """One inner epoch over a shuffled buffer: every micro-step in order (T:755-861), batched per accumulation
-        window up to `max_pass_images` images per UNet pass."""
+        window up to `max_pass_images` images per UNet pass.  Python's cyclic garbage collector is paused for the
+        epoch (PSO_GC_PAUSE=0 keeps it running): the ~3k kernel launches of a step allocate enough small objects to
+        trigger collections in the middle of launch-bound stretches."""
+        gc_on = _GC_PAUSE and gc.isenabled()
+        if gc_on:
+            gc.disable()
+        try:
+            self._train_epoch(sb, generator)
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def _train_epoch(self, sb, generator=None):
         s = 0
         per_pass = max(1, self.max_pass_images // (2 * self.P))
         while s < sb.n_micro:
