@@ -15,10 +15,12 @@ Secondary objects on the same JSON line (never the headline value):
               reference UNet, 1 pair per micro-step -- its own warmed-up, timed steps + dominant-kernel roofline;
   "lora_bs1"  the north-star operating point "bs = 1 / GPU": the C2 LoRA step at 1 pair, gas 1 (one micro-step =
               2 policy + 2 reference images in one paired pass);
+  "c5"        BASELINE configs[4] on this GPU: the DreamBooth PSO micro-step (1 instance + 1 negative, r = 16, VAE
+              encode in the step), bf16 and with the fp8 forward, and their ratio;
   "dist"      (N > 1) the backend and world size torch.distributed really runs, every rank's ms/step, and the
               bucketed all-reduce: bytes on the wire, its time alone, and the part of it left exposed after the
               backward (the rest ran under the backward).
-  Both config objects run at N = 1 only (--no-extra skips them).
+  The config objects run at N = 1 only (--no-extra skips them).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
   Under torchrun (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one rank.  Started directly with --gpus N > 1,
@@ -70,7 +72,7 @@ def parse():
                     help="fp32 AdamW instead of the reference default 8-bit AdamW (config use_8bit_adam = True)")
     ap.add_argument("--allreduce-bf16", action="store_true",
                     help="bf16 gradient all-reduce (fp32 accumulation and optimizer; half the xGMI bytes)")
-    ap.add_argument("--no-extra", action="store_true", help="skip the c3 / lora_bs1 secondary objects")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c3 / lora_bs1 / c5 secondary objects")
     ap.add_argument("--extra-steps", type=int, default=3)
     return ap.parse_args()
 
@@ -293,6 +295,51 @@ def sub_config(args, dev, name, steps, warmup=1, **over):
     return out
 
 
+def c5_metric(dev, steps=8, warmup=2):
+    """BASELINE configs[4] on this GPU: the DreamBooth PSO micro-step (pso_db, LoRA r = 16, 1 instance + 1 negative
+    image, VAE encode inside the step, gas 4 -- the recipe's batch) at 1024^2, bf16 and with the fp8 forward of the
+    cross-attention q / GEGLU proj (enable_fp8_forward), same model, same inputs."""
+    from types import SimpleNamespace
+    from pairwise_sample_optimization_amd.dreambooth import DreamBoothPSOTrainer
+    from pairwise_sample_optimization_amd.trainer import compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    from pairwise_sample_optimization_amd.vae import AutoencoderKL
+    with torch.device(dev):
+        unet = UNet2DConditionModel(UNetConfig.sdxl(128))
+        vae = AutoencoderKL()
+    unet.init_weights(0)
+    vae.init_weights(1)
+    unet.add_adapter(SimpleNamespace(r=16, lora_alpha=16))
+    unet.lora.init_gaussian(seed=0, b_std=1e-3)
+    unet.prepare()
+    tr = DreamBoothPSOTrainer(unet, vae, loss_type="pso_db", beta_pso=5.0, gradient_accumulation_steps=4)
+    g = torch.Generator(device=dev).manual_seed(0)
+    pix = torch.rand(2, 3, 1024, 1024, device=dev, generator=g) * 2 - 1
+    enc = torch.randn(1, 77, 2048, device=dev, generator=g).bfloat16()
+    pooled = torch.randn(1, 1280, device=dev, generator=g).bfloat16()
+    tid = compute_time_ids(1024, 0, dev)
+    out = {}
+    for fp8 in (False, True):
+        unet.enable_fp8_forward(fp8)
+        for _ in range(warmup):
+            tr.micro_step(pix, enc, pooled, tid, generator=g)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.micro_step(pix, enc, pooled, tid, generator=g)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        out["fp8" if fp8 else "bf16"] = {"imgs_per_s": round(2 / dt, 3), "ms_per_micro_step": round(dt * 1e3, 2)}
+    unet.enable_fp8_forward(False)
+    out["fp8_over_bf16"] = round(out["fp8"]["imgs_per_s"] / out["bf16"]["imgs_per_s"], 4)
+    out["workload"] = ("C5 (1 GPU): DreamBooth PSO pso_db, SDXL-Turbo UNet + VAE encoder, LoRA r=16, 1 instance + 1 "
+                       "negative per micro-step, gas 4, 1024^2; fp8 = e4m3 cross-attention q and GEGLU proj, bf16 backward")
+    del unet, vae, tr
+    torch.cuda.empty_cache()
+    log(f"[bench] c5: bf16 {out['bf16']['imgs_per_s']} / fp8 {out['fp8']['imgs_per_s']} imgs/s")
+    return out
+
+
 def dist_report(tr, dev, dt_rank, steps):
     """What torch.distributed really ran (backend, world) and the overlap of the gradient all-reduce with the
     backward: exposed = the compute stream's wait for RCCL after the window's last backward (GradBuckets.finish,
@@ -431,6 +478,8 @@ def main():
                                     gas=1, full_unet=True),
                          workload="C3: SDXL-DMD2 PSO, 4-step sampler (T=3), full-UNet grads vs a frozen reference UNet, "
                                   "1 pair / micro-step, gas 1, bf16, 1024^2")
+        log("[bench] c5 ...")
+        res["c5"] = c5_metric(dev)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

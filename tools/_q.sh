@@ -1,1 +1,1 @@
-AB_ARGS="--pairs 1 --gas 1" bash tools/ab.sh env "PSO_GC_PAUSE=1 PSO_GC_PAUSE=0" 3 > gpurun_out/ab_gc_bs1.log 2>&1 && bash tools/ab.sh env "PSO_GC_PAUSE=1 PSO_GC_PAUSE=0" 2 > gpurun_out/ab_gc_c2.log 2>&1
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; echo rc=$?; tail -3 gpurun_out/bench.err
