@@ -871,9 +871,9 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
-// the variants 37-52 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
-// 256 x 160 8-phase tiles off / forced; ...); any other non-zero variant forces one tile shape
-static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 52) ? 0 : gv_raw; }
+// the variants 37-56 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// 256 x 160 8-phase tiles off / forced; 56 = the 256 x 256 TN tiles off; ...); any other non-zero variant forces one tile shape
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 56) ? 0 : gv_raw; }
 // the workspace split-K forms (pso_gemm_ws / pso_conv2d_ws) under the benchmark knobs: off where a variant forces a
 // tile (38 / 39 / 44: the 8-phase 256 x 160 / 256 x 320 / conv tiles, the tests that pin them), where a raster group
 // is forced, and under variant 52 (the conv split off)
@@ -1331,6 +1331,159 @@ __global__ void tn_reduce_slices_kernel(int I, int J, int ks, const float* __res
   o[0] += sacc.x; o[1] += sacc.y; o[2] += sacc.z; o[3] += sacc.w;
 }
 
+// 256 x 256 TN tile for the large full-weight gradients: 8 waves of 64 x 128 (4 x 8 MFMA tiles; each A fragment
+// feeds 8 MFMAs, each B fragment 4), the same per-wave 64 x 64 images and transposed reads as gemm_tn128_kernel.  A
+// 128 x 128 tile moves 32 KB of operands per 2.1 MFLOP (one 64-token step) -- ~38 TB/s of L2 reads at the MFMA peak
+// over 256 CUs, more than the L2s deliver; the 256 x 256 tile halves the bytes per flop.  One workgroup per CU
+// (128 KB LDS: 2 stages x 8 images).  part != nullptr: this slice's partial product into the workspace (ordered
+// reduction by tn_reduce_slices_kernel); else out += directly (the caller launches one slice).
+__global__ __launch_bounds__(512, 1) void gemm_tn256_kernel(int M, int I, int J, const bf16_t* __restrict__ A,
+                                                            long lda, const bf16_t* __restrict__ B, long ldb,
+                                                            float alpha, float* __restrict__ out, long ldo,
+                                                            int steps, float* __restrict__ part, int geglu_f) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t t256s[];  // [stage][A0 A1 A2 A3 B0 B1 B2 B3][64 x 64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
+  const int g = lane >> 4, c = lane & 15;
+  const int nbj = (J + 255) / 256;
+  const int bi = blockIdx.x / nbj, bj = blockIdx.x - bi * nbj;
+  const int i0 = bi * 256, j0 = bj * 256;
+  const int nkt = (M + 63) / 64;
+  const int t_beg = blockIdx.y * steps, t_end = min(nkt, t_beg + steps);
+  // wave w stages image w: A columns i0 + 64 w (w < 4) or B columns j0 + 64 (w - 4), 8 pieces of 8 rows x 128 B
+  const bool isA = wave < 4;
+  const long ld = isA ? lda : ldb;
+  const int col0 = (isA ? i0 : j0) + (wave & 3) * 64;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(isA ? A : B), (short)0, (int)(((long)(M - 1) * ld + (isA ? I : J)) * 2), 0x00020000);
+  const int prow = lane >> 3, pch = lane & 7;
+  const int sc = pch ^ (((prow >> 1) & 3) << 1);
+  const int cw = min(col0 + sc * 8, (isA ? I : J) - 8);
+  const unsigned voff = (unsigned)((long)prow * ld + cw) * 2u;
+  const int kstep = (int)(64 * ld * 2);
+  auto issue = [&](int t, int stg) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (tnr_lds_void_g*)(t256s + (stg * 8 + wave) * 4096 + p * 8 * 64), 16,
+                                               voff + (unsigned)(p * 8 * ld * 2), t * kstep, 0, 0);
+  };
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned lbase = (unsigned)(uintptr_t)(const tnr_lds_void_g*)t256s;
+  if (t_beg < t_end) issue(t_beg, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int t = t_beg; t < t_end; ++t) {
+    const int cur = (t - t_beg) & 1;
+    if (t + 1 < t_end) issue(t + 1, cur ^ 1);
+    const unsigned ia = lbase + (unsigned)((cur * 8 + wi) * 4096 * 2);
+    const unsigned ib = lbase + (unsigned)((cur * 8 + 4 + 2 * wj) * 4096 * 2);  // images 4 + 2 wj, 5 + 2 wj
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s16x4 ra[8], rb[16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        ra[2 * a] = tn_tr_asm(ia, ks * 32 + 8 * g, a * 16, lane);
+        ra[2 * a + 1] = tn_tr_asm(ia, ks * 32 + 8 * g + 4, a * 16, lane);
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const unsigned im = ib + (unsigned)((b >> 2) * 4096 * 2);
+        rb[2 * b] = tn_tr_asm(im, ks * 32 + 8 * g, (b & 3) * 16, lane);
+        rb[2 * b + 1] = tn_tr_asm(im, ks * 32 + 8 * g + 4, (b & 3) * 16, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(ra[0]), "+v"(ra[1]), "+v"(ra[2]), "+v"(ra[3]), "+v"(ra[4]), "+v"(ra[5]), "+v"(ra[6]),
+                     "+v"(ra[7]), "+v"(rb[0]), "+v"(rb[1]), "+v"(rb[2]), "+v"(rb[3]));
+      asm volatile(""
+                   : "+v"(rb[4]), "+v"(rb[5]), "+v"(rb[6]), "+v"(rb[7]), "+v"(rb[8]), "+v"(rb[9]), "+v"(rb[10]),
+                     "+v"(rb[11]), "+v"(rb[12]), "+v"(rb[13]), "+v"(rb[14]), "+v"(rb[15]));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      bf16x8 af[4], bfr[8];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        s16x8 va = {ra[2 * a][0], ra[2 * a][1], ra[2 * a][2], ra[2 * a][3],
+                    ra[2 * a + 1][0], ra[2 * a + 1][1], ra[2 * a + 1][2], ra[2 * a + 1][3]};
+        af[a] = __builtin_bit_cast(bf16x8, va);
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        s16x8 vb = {rb[2 * b][0], rb[2 * b][1], rb[2 * b][2], rb[2 * b][3],
+                    rb[2 * b + 1][0], rb[2 * b + 1][1], rb[2 * b + 1][2], rb[2 * b + 1][3]};
+        bfr[b] = __builtin_bit_cast(bf16x8, vb);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // lane holds out[i = i0 + wi*64 + a*16 + c][j = j0 + wj*128 + b*16 + 4g + r]
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = i0 + wi * 64 + a * 16 + c;
+    if (i >= I) continue;
+    const int io = geglu_f > 0 ? ((i >> 6) << 5) + (i & 31) + ((i & 32) ? geglu_f : 0) : i;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int j = j0 + wj * 128 + b * 16 + 4 * g;
+      if (j >= J) continue;
+      if (part) {
+        *reinterpret_cast<float4*>(part + ((long)blockIdx.y * I + i) * J + j) =
+            make_float4(acc[a][b][0] * alpha, acc[a][b][1] * alpha, acc[a][b][2] * alpha, acc[a][b][3] * alpha);
+      } else {
+        float* o = out + (long)io * ldo + j;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] += acc[a][b][r] * alpha;
+      }
+    }
+  }
+}
+
+// the 256 x 256 TN tiles (variant 56 keeps the 128 x 128 ones): both sides multiples of 256 and the operands within
+// 32-bit buffer offsets.  Returns the slice count: 1 where the tiles alone cover >= 3/4 of the CUs (out += directly);
+// one round of workspace slices of >= 8 K-steps each where the 128 x 128 tiles would run one pass of 256-383
+// workgroups (< 3/4 of the two-per-CU slots, and too many for tn_ws_slices); else 0 = not this kernel.
+// tools/tn_full_bench.py, TF/s 256 vs 128 tiles: 6144 x 1280 x 11520 (225 tiles) 948 / 929 vs 835 / 836, 24576 x 1280
+// x 11520 990 vs 823, the GEGLU 6144 x 10240 x 1280 (200 tiles) 720 / 736 vs 658 / 725, 6144 x 3840 x 1280 (75 tiles x
+// 3 slices) 675 / 683 vs 607 / 616; slices where the 128 x 128 tiles already fill the slots lose (6144 x 1280 x 5120,
+// 100 tiles x 2: 670 vs 752; 6144 x 1280 x 1280, 25 x 10: 411 vs 471): the partials' round trip through HBM.
+static int tn256_slices(int M, int I, int J, long lda, long ldb) {
+  if (g_gemm_variant == 56 || I % 256 || J % 256 || (long)M * lda >= (1L << 30) || (long)M * ldb >= (1L << 30))
+    return 0;
+  const int t256 = (I / 256) * (J / 256);
+  if (t256 >= 192) return 1;
+  const int t128 = (I / 128) * (J / 128);
+  if (t128 < 256 || t128 >= 384) return 0;
+  const int nkt = (M + 63) / 64;
+  int ks = 256 / t256;
+  if (ks > nkt / 8) ks = nkt / 8;
+  if (ks < 2) return 0;
+  const int steps = (nkt + ks - 1) / ks;
+  return (nkt + steps - 1) / steps;
+}
+
+static void tn256_launch(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
+                         long ldo, int ks, float* part, int geglu_f, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_tn256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    return true;
+  }();
+  (void)attr;
+  const int nkt = (M + 63) / 64;
+  const int steps = (nkt + ks - 1) / ks;
+  pso_note_kernel("gemm_tn256_kernel");
+  gemm_tn256_kernel<<<dim3((I / 256) * (J / 256), ks), 512, 131072, st>>>(M, I, J, (const bf16_t*)A, lda,
+                                                                          (const bf16_t*)B, ldb, alpha, out, ldo,
+                                                                          steps, part, geglu_f);
+}
+
 // split of the full-weight TN product into ks slices of the reduction rows for the workspace form: enough slices for
 // ~1.5 rounds of 128 x 128 tiles over the 256 CUs, each slice >= 8 K-steps (512 rows)
 static int tn_ws_slices(int M, int I, int J) {
@@ -1350,7 +1503,8 @@ static int tn_ws_slices(int M, int I, int J) {
 //              split the atomic form would take)
 //   TNP_64:    the rest -> 64 x 64 tiles, ks slices
 //   TNP_PLAIN: no split: out += directly (deterministic as it stands)
-enum { TNP_PLAIN = 0, TNP_RANK = 1, TNP_128 = 2, TNP_64 = 3 };
+//   TNP_256:   both sides multiples of 256 with too few tiles for the CUs -> 256 x 256 tiles, one round of slices
+enum { TNP_PLAIN = 0, TNP_RANK = 1, TNP_128 = 2, TNP_64 = 3, TNP_256 = 4 };
 struct TnPlan { int kind, ks, steps; size_t bytes; };
 static bool tn_rank_ok(int r) { return r == 16 || r == 32 || r == 64 || r == 96; }
 static TnPlan tn_plan(int M, int I, int J, long lda, long ldb) {
@@ -1366,6 +1520,15 @@ static TnPlan tn_plan(int M, int I, int J, long lda, long ldb) {
     return p;
   }
   const int nkt = (M + 63) / 64;
+  const int ks256 = tn256_slices(M, I, J, lda, ldb);
+  if (ks256 == 1) return p;  // the direct 256 x 256 form (pso_gemm_tn_grouped)
+  if (ks256 >= 2) {
+    p.kind = TNP_256;
+    p.ks = ks256;
+    p.steps = (nkt + ks256 - 1) / ks256;
+    p.bytes = (size_t)ks256 * I * J * sizeof(float);
+    return p;
+  }
   if (I >= 128 && J >= 128 && (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30)) {
     int ks = tn_ws_slices(M, I, J);
     if (!ks) {  // the split the atomic form takes (pso_gemm_tn_grouped): ks <= M / 16384 where it yields >= 128 blocks
@@ -1419,9 +1582,11 @@ int pso_gemm_tn_ws(int M, int I, int J, const void* A, long lda, const void* B, 
     q.out = out; q.ldo = ldo; q.M = M; q.C = x_is_a ? I : J; q.group_c = 0; q.alpha = alpha;
     return pso_gemm_tn_rank_batch_ws(x_is_a ? J : I, x_is_a ? 0 : 1, 1, &q, ws, ws_bytes, stream);
   }
-  if ((p.kind == TNP_128 || p.kind == TNP_64) && ws_ok) {
+  if ((p.kind == TNP_128 || p.kind == TNP_64 || p.kind == TNP_256) && ws_ok) {
     const long n4 = (long)I * J / 4;
-    if (p.kind == TNP_128) {
+    if (p.kind == TNP_256) {
+      tn256_launch(M, I, J, A, lda, B, ldb, alpha, out, ldo, p.ks, (float*)ws, 0, st);
+    } else if (p.kind == TNP_128) {
       const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
       pso_note_kernel("gemm_tn128_kernel");
       gemm_tn128_kernel<<<dim3(t128, p.ks), 256, 0, st>>>(M, I, J, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, alpha,
@@ -1710,6 +1875,10 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   }
   PSO_ARG_CHECK(group == 0, "pso_gemm_tn: grouped form needs a rank-32/64/96 side and 128 | group");
   const int nkt = (M + 63) / 64;
+  if (g_tn_split == 0 && tn256_slices(M, I, J, lda, ldb) == 1) {
+    tn256_launch(M, I, J, A, lda, B, ldb, alpha, out, ldo, 1, nullptr, 0, (hipStream_t)stream);
+    return pso_check_launch("pso_gemm_tn");
+  }
   // full-weight gradients (both sides >= 128 wide): 128 x 128 tiles; split over M only as far as needed to cover ~2
   // rounds of co-resident blocks (each split adds its tile of f32 atomics)
   static const int tn128 = [] {
@@ -1756,6 +1925,10 @@ int pso_gemm_tn_geglu(int M, int F2, int J, const void* A, long lda, const void*
   PSO_ARG_CHECK((long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30), "pso_gemm_tn_geglu: operand too large");
   if (M == 0) return PSO_OK;
   // one pass over the reduction rows (no split: += straight into the natural-order gradient, deterministic)
+  if (tn256_slices(M, F2, J, lda, ldb) == 1) {
+    tn256_launch(M, F2, J, A, lda, B, ldb, alpha, out, ldo, 1, nullptr, F2 / 2, (hipStream_t)stream);
+    return pso_check_launch("pso_gemm_tn_geglu");
+  }
   const int t128 = (F2 / 128) * ((J + 127) / 128);
   pso_note_kernel("gemm_tn128_kernel");
   gemm_tn128_kernel<<<dim3(t128, 1), 256, 0, (hipStream_t)stream>>>(M, F2, J, (const bf16_t*)A, lda, (const bf16_t*)B,

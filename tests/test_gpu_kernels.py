@@ -165,12 +165,15 @@ def test_conv_stride1_input_grad_flipped(cuda):
                                    (1000, 640, 64), (616, 1280, 32), (77, 32, 256),
                                    # full-weight gradients (128 x 128 TN tiles): ragged M / I / J, split-K atomics
                                    (16384, 1280, 1280), (1000, 640, 320), (616, 2880, 640), (77, 136, 264),
-                                   (16384, 128, 128), (4100, 1152, 320)])
+                                   (16384, 128, 128), (4100, 1152, 320),
+                                   # 256 x 256 TN tiles: one round of workspace slices, and direct (>= 192 tiles)
+                                   (6144, 3840, 1280), (1000, 3840, 1280), (2100, 2048, 2048), (3000, 4096, 3072)])
 @pytest.mark.parametrize("split_ws", [True, False])
 def test_gemm_tn_vs_fp32(cuda, M, I, J, split_ws):
     """Generic TN path and the streaming rank-r path (one side 32 / 64 / 96 wide), partial 64-row steps included;
     full-weight shapes with few 128 x 128 tiles through the workspace split (pso_gemm_tn_ws: partial products stored
-    per row slice, added in slice order) and, split_ws=False, through pso_gemm_tn (f32-atomic split)."""
+    per row slice, added in slice order) and, split_ws=False, through pso_gemm_tn (f32-atomic split); sides that are
+    multiples of 256 on the 256 x 256 tiles (workspace slices, or one direct pass with >= 192 tiles)."""
     from pairwise_sample_optimization_amd import kernels as K_
     big = torch.randn(M, I + 16, device=cuda).bfloat16()
     a = big[:, 8:8 + I]          # column-slice view (row stride != I)
