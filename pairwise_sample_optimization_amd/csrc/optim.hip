@@ -11,6 +11,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -95,6 +96,7 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
 // kOptimizerStatic8bit2StateBlockwise ADAM branch (restated in oracle/adam8bit.py, parity unpinned: no bitsandbytes
 // here), contraction off so the fp32 rounding matches the restatement step for step.
 #define ADAM8_BLOCK 2048
+#define ADAM8_LAYOUT_DEFAULT 1  // element-to-thread mapping of the 8-bit AdamW (adamw8bit_kernel<LAY>)
 struct Adam8Maps {
   float s[256], u[256];
 };
@@ -137,14 +139,15 @@ __device__ __forceinline__ int adam8_node(int i) {
 // m32 / v32 + desc[4b+2] + (i - start).  desc == nullptr: uniform 2048-element blocks over [0, n), all 8-bit.
 // Non-finite gradient elements leave the parameter, m and v unchanged (bitsandbytes skips the parameter update for
 // them; its state update for such an element is not pinned here).
-__global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
-                                                        uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
-                                                        float* __restrict__ am, float* __restrict__ av, float b1,
-                                                        float omb1, float b2, float omb2, float eps_c2, float step_size,
-                                                        float decay, float gscale, const float* __restrict__ clip,
-                                                        bf16_t* __restrict__ pw, const long* __restrict__ desc,
-                                                        float* __restrict__ m32, float* __restrict__ v32,
-                                                        Adam8Maps maps) {
+// LAY = element-to-thread mapping inside a block.  0: thread t owns the 8 consecutive elements 8t .. 8t + 7 (each
+// 16-B access instruction of a wave spans 2 KB with 16-B gaps); 1: thread t owns 4t .. 4t + 3 and 1024 + 4t .. +3, so
+// every access instruction of a wave covers one contiguous range.  Per-block results are the same bits either way.
+template <int LAY>
+__global__ __launch_bounds__(256) void adamw8bit_kernel(
+    long n, float* __restrict__ p, const float* __restrict__ g, uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
+    float* __restrict__ am, float* __restrict__ av, float b1, float omb1, float b2, float omb2, float eps_c2,
+    float step_size, float decay, float gscale, const float* __restrict__ clip, bf16_t* __restrict__ pw,
+    const long* __restrict__ desc, float* __restrict__ m32, float* __restrict__ v32, Adam8Maps maps) {
 #pragma clang fp contract(off)
   __shared__ float cs[256], cu[256], ts[256], tu[256];
   __shared__ float red[2][4];
@@ -165,44 +168,44 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
       tu[adam8_node(t)] = maps.u[t];
     }
   }
-  const long i0 = base + (long)t * 8;
-  // 32-B / 8-B vector accesses wherever the thread's 8 elements are whole and aligned
-  const bool full = i0 + 8 <= end && (base & 7) == 0 && (!st32 || (soff & 3) == 0);
+  // the thread's two 4-element chunks: elements e < 4 at o0 + e, e >= 4 at o1 + e - 4
+  const long o0 = LAY ? base + 4L * t : base + 8L * t;
+  const long o1 = LAY ? o0 + ADAM8_BLOCK / 2 : o0 + 4;
+  auto at = [&](int e) { return (e < 4 ? o0 : o1) + (e & 3); };
+  // 16-B / 4-B vector accesses wherever both chunks are whole and aligned
+  const bool full = o0 + 4 <= end && o1 + 4 <= end && (base & 3) == 0 && (!st32 || (soff & 3) == 0);
   const float s = gscale * (clip ? clip[1] : 1.0f);
   float gv[8], pv[8];
   if (full) {
-    const float4 g0 = *reinterpret_cast<const float4*>(g + i0), g1 = *reinterpret_cast<const float4*>(g + i0 + 4);
-    const float4 p0 = *reinterpret_cast<const float4*>(p + i0), p1 = *reinterpret_cast<const float4*>(p + i0 + 4);
+    const float4 g0 = *reinterpret_cast<const float4*>(g + o0), g1 = *reinterpret_cast<const float4*>(g + o1);
+    const float4 p0 = *reinterpret_cast<const float4*>(p + o0), p1 = *reinterpret_cast<const float4*>(p + o1);
     gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w; gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
     pv[0] = p0.x; pv[1] = p0.y; pv[2] = p0.z; pv[3] = p0.w; pv[4] = p1.x; pv[5] = p1.y; pv[6] = p1.z; pv[7] = p1.w;
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const long i = i0 + e;
+      const long i = at(e);
       gv[e] = i < end ? g[i] : 0.f;
       pv[e] = i < end ? p[i] : 0.f;
     }
   }
   if (st32) {  // bitsandbytes 32-bit state (kOptimizer32bit2State ADAM): same arithmetic, no quantisation
-    float* ms = m32 + soff + (i0 - base);
-    float* vs = v32 + soff + (i0 - base);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      if (!(full || i0 + e < end)) continue;
-      const float gi = gv[e] * s;
-      if (!isfinite(gi)) continue;
-      float m = ms[e], v = vs[e];
-      m = (m * b1) + (omb1 * gi);
-      v = (v * b2) + ((omb2 * gi) * gi);
-      ms[e] = m;
-      vs[e] = v;
-      pv[e] = pv[e] + (step_size * (m / (sqrtf(v) + eps_c2)));
-      pv[e] = pv[e] * decay;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const long i = i0 + e;
+      const long i = at(e);
       if (i >= end) continue;
+      const float gi = gv[e] * s;
+      if (isfinite(gi)) {
+        float* ms = m32 + soff + (i - base);
+        float* vs = v32 + soff + (i - base);
+        float m = *ms, v = *vs;
+        m = (m * b1) + (omb1 * gi);
+        v = (v * b2) + ((omb2 * gi) * gi);
+        *ms = m;
+        *vs = v;
+        pv[e] = pv[e] + (step_size * (m / (sqrtf(v) + eps_c2)));
+        pv[e] = pv[e] * decay;
+      }
       p[i] = pv[e];
       if (pw) pw[i] = f2bf(pv[e]);
     }
@@ -211,13 +214,15 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   const float am0 = am[blk], av0 = av[blk];
   uint32_t cm[2], cv[2];
   if (full) {
-    const uint2 qa = *reinterpret_cast<const uint2*>(qm + i0), qb = *reinterpret_cast<const uint2*>(qv + i0);
-    cm[0] = qa.x; cm[1] = qa.y; cv[0] = qb.x; cv[1] = qb.y;
+    cm[0] = *reinterpret_cast<const uint32_t*>(qm + o0);
+    cm[1] = *reinterpret_cast<const uint32_t*>(qm + o1);
+    cv[0] = *reinterpret_cast<const uint32_t*>(qv + o0);
+    cv[1] = *reinterpret_cast<const uint32_t*>(qv + o1);
   } else {
     cm[0] = cm[1] = cv[0] = cv[1] = 0u;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const long i = i0 + e;
+      const long i = at(e);
       if (i < end) {
         cm[e >> 2] |= (uint32_t)qm[i] << (8 * (e & 3));
         cv[e >> 2] |= (uint32_t)qv[i] << (8 * (e & 3));
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   float mx_m = 0.f, mx_v = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    if (full || i0 + e < end) {
+    if (full || at(e) < end) {
       const float gi = gv[e] * s;
       m[e] = cs[(cm[e >> 2] >> (8 * (e & 3))) & 255u] * am0;
       v[e] = cu[(cv[e >> 2] >> (8 * (e & 3))) & 255u] * av0;
@@ -265,22 +270,24 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(long n, float* __restric
   adam8_nearest(cs, ts, xm, im);
   adam8_nearest(cu, tu, xv, iv);
   if (full) {
-    *reinterpret_cast<float4*>(p + i0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
-    *reinterpret_cast<float4*>(p + i0 + 4) = make_float4(pv[4], pv[5], pv[6], pv[7]);
-    if (pw) {  // the bf16 working copy of the parameters (round to nearest even), 16-B store
-      *reinterpret_cast<uint4*>(pw + i0) =
-          make_uint4(pack2bf(pv[0], pv[1]), pack2bf(pv[2], pv[3]), pack2bf(pv[4], pv[5]), pack2bf(pv[6], pv[7]));
+    *reinterpret_cast<float4*>(p + o0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    *reinterpret_cast<float4*>(p + o1) = make_float4(pv[4], pv[5], pv[6], pv[7]);
+    if (pw) {  // the bf16 working copy of the parameters (round to nearest even)
+      *reinterpret_cast<uint2*>(pw + o0) = make_uint2(pack2bf(pv[0], pv[1]), pack2bf(pv[2], pv[3]));
+      *reinterpret_cast<uint2*>(pw + o1) = make_uint2(pack2bf(pv[4], pv[5]), pack2bf(pv[6], pv[7]));
     }
-    *reinterpret_cast<uint2*>(qm + i0) =
-        make_uint2((uint32_t)im[0] | (uint32_t)im[1] << 8 | (uint32_t)im[2] << 16 | (uint32_t)im[3] << 24,
-                   (uint32_t)im[4] | (uint32_t)im[5] << 8 | (uint32_t)im[6] << 16 | (uint32_t)im[7] << 24);
-    *reinterpret_cast<uint2*>(qv + i0) =
-        make_uint2((uint32_t)iv[0] | (uint32_t)iv[1] << 8 | (uint32_t)iv[2] << 16 | (uint32_t)iv[3] << 24,
-                   (uint32_t)iv[4] | (uint32_t)iv[5] << 8 | (uint32_t)iv[6] << 16 | (uint32_t)iv[7] << 24);
+    *reinterpret_cast<uint32_t*>(qm + o0) =
+        (uint32_t)im[0] | (uint32_t)im[1] << 8 | (uint32_t)im[2] << 16 | (uint32_t)im[3] << 24;
+    *reinterpret_cast<uint32_t*>(qm + o1) =
+        (uint32_t)im[4] | (uint32_t)im[5] << 8 | (uint32_t)im[6] << 16 | (uint32_t)im[7] << 24;
+    *reinterpret_cast<uint32_t*>(qv + o0) =
+        (uint32_t)iv[0] | (uint32_t)iv[1] << 8 | (uint32_t)iv[2] << 16 | (uint32_t)iv[3] << 24;
+    *reinterpret_cast<uint32_t*>(qv + o1) =
+        (uint32_t)iv[4] | (uint32_t)iv[5] << 8 | (uint32_t)iv[6] << 16 | (uint32_t)iv[7] << 24;
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const long i = i0 + e;
+      const long i = at(e);
       if (i >= end) continue;
       p[i] = pv[e];
       if (pw) pw[i] = f2bf(pv[e]);
@@ -401,10 +408,21 @@ static int adam8_launch(long n, int nblk, float* param, void* param_bf16, const 
   const float step_size = (-lr) * c2 / c1;
   const float decay = (float)(1.0 - (double)lr * weight_decay);
   if (nblk <= 0) return PSO_OK;
-  adamw8bit_kernel<<<nblk, 256, 0, (hipStream_t)stream>>>(n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v,
-                                                           beta1, (float)(1.0 - b1), beta2, (float)(1.0 - b2),
-                                                           c2 * eps, step_size, decay, grad_scale, clip_coef,
-                                                           (bf16_t*)param_bf16, desc, m32, v32, maps);
+  // element layout inside a block: PSO_ADAM8_LAYOUT (0 / 1) for the benchmark
+  static const int lay = [] {
+    const char* e = getenv("PSO_ADAM8_LAYOUT");
+    return e ? (atoi(e) != 0) : ADAM8_LAYOUT_DEFAULT;
+  }();
+  const hipStream_t st = (hipStream_t)stream;
+  const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2);
+#define PSO_ADAM8_ARGS                                                                                                   \
+  n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, beta1, omb1, beta2, omb2, c2 * eps, step_size, decay,     \
+      grad_scale, clip_coef, (bf16_t*)param_bf16, desc, m32, v32, maps
+  if (lay)
+    adamw8bit_kernel<1><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
+  else
+    adamw8bit_kernel<0><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
+#undef PSO_ADAM8_ARGS
   return pso_check_launch("pso_adamw8bit_step");
 }
 
