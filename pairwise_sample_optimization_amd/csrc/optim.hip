@@ -110,16 +110,19 @@ struct Adam8Maps {
 template <int NV>
 __device__ __forceinline__ void adam8_nearest(const float* __restrict__ code, const float* __restrict__ tree,
                                               const float (&x)[NV], int (&idx)[NV]) {
-  int nd[NV];
+  // the descent tracks the node's byte offset (4 * node): compare, select, shift-add per level (no separate index to
+  // address shift)
+  const char* tb = reinterpret_cast<const char*>(tree);
+  unsigned a[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) nd[k] = 1;
+  for (int k = 0; k < NV; ++k) a[k] = 4u;
 #pragma unroll
   for (int d = 0; d < 8; ++d)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) nd[k] = 2 * nd[k] + (tree[nd[k]] < x[k] ? 1 : 0);
+    for (int k = 0; k < NV; ++k) a[k] = (a[k] << 1) + (*reinterpret_cast<const float*>(tb + a[k]) < x[k] ? 4u : 0u);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const int lo = nd[k] - 256;
+    const int lo = (int)(a[k] >> 2) - 256;
     const int i = lo < 1 ? 1 : lo;
     const float a = code[i - 1], b = code[i];
     idx[k] = fabsf(x[k] - a) <= fabsf(b - x[k]) ? i - 1 : i;
