@@ -241,12 +241,14 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(
       const float gi = gv[e] * s;
       m[e] = cs[(cm[e >> 2] >> (8 * (e & 3))) & 255u] * am0;
       v[e] = cu[(cv[e >> 2] >> (8 * (e & 3))) & 255u] * av0;
-      if (isfinite(gi)) {
-        m[e] = (m[e] * b1) + (omb1 * gi);
-        v[e] = (v[e] * b2) + ((omb2 * gi) * gi);
-        pv[e] = pv[e] + (step_size * (m[e] / (sqrtf(v[e]) + eps_c2)));
-        pv[e] = pv[e] * decay;
-      }
+      // branch-free: a non-finite gradient element keeps p, m and v (the update is computed and discarded)
+      const bool fin = isfinite(gi);
+      const float m1 = (m[e] * b1) + (omb1 * gi);
+      const float v1 = (v[e] * b2) + ((omb2 * gi) * gi);
+      const float p1 = (pv[e] + (step_size * (m1 / (sqrtf(v1) + eps_c2)))) * decay;
+      m[e] = fin ? m1 : m[e];
+      v[e] = fin ? v1 : v[e];
+      pv[e] = fin ? p1 : pv[e];
       mx_m = fmaxf(mx_m, fabsf(m[e]));
       mx_v = fmaxf(mx_v, fabsf(v[e]));
     } else {

@@ -3,7 +3,7 @@ HBM rate on its 18 B per parameter (fp32 param read + write, fp32 grad read, two
 working copy written).  Round 4: 11.8 ms over 2.567e9 parameters (3.9 TB/s); a persistent form (4 / 6 / 8
 workgroups per CU walking the blocks, the maps loaded once per workgroup) ran 14.7 / 13.8 / 13.5 ms; 2 / 4 blocks per
 workgroup 12.1 / 12.4 vs 11.9 ms; the contiguous element layout (PSO_ADAM8_LAYOUT=1, now the default) 11.44 / 11.50
-vs 11.88 / 11.96 ms on one box, same bits.
+vs 11.88 / 11.96 ms on one box, same bits; byte-offset search 10.86, branch-free non-finite skip 10.50 ms.
 usage (GPU): python tools/adam8_bench.py [n_params]"""
 import os
 import sys
