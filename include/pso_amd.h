@@ -432,6 +432,13 @@ int pso_adamw8bit_step_blocks(long n, int nblk, const long* desc, float* param, 
                               uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v,
                               float* exp_avg_32, float* exp_avg_sq_32, float lr, float beta1, float beta2, float eps,
                               float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream);
+/* = pso_adamw8bit_step_blocks, and every gradient element a block covers is zeroed once it has been read
+ * (optimizer.zero_grad, T:861, folded into the step: no separate pass over the gradient).  Pads are not touched. */
+int pso_adamw8bit_step_blocks_zero_grad(long n, int nblk, const long* desc, float* param, void* param_bf16,
+                                        float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m,
+                                        float* absmax_v, float* exp_avg_32, float* exp_avg_sq_32, float lr,
+                                        float beta1, float beta2, float eps, float weight_decay, int step,
+                                        float grad_scale, const float* clip_coef, void* stream);
 int pso_zero_f32(long n, float* x, void* stream);
 int pso_preference(int P, int m, const float* rewards, const int64_t* reward_idx, int mode, float* pref,
                    void* stream);

@@ -126,6 +126,8 @@ SIGNATURES = {
     "pso_adamw8bit_step_bf16": (ci, [cl, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf, vp, vp]),
     "pso_adamw8bit_step_blocks": (ci, [cl, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf, ci, cf,
                                        vp, vp]),
+    "pso_adamw8bit_step_blocks_zero_grad": (ci, [cl, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cf, cf, cf, cf, cf,
+                                                 ci, cf, vp, vp]),
     "pso_zero_f32": (ci, [cl, vp, vp]),
     "pso_preference": (ci, [ci, ci, vp, vp, ci, vp, vp]),
     "pso_nhwc_to_nchw": (ci, [ci, ci, cl, vp, vp, ci, vp]),

@@ -147,10 +147,10 @@ __device__ __forceinline__ int adam8_node(int i) {
 // every access instruction of a wave covers one contiguous range.  Per-block results are the same bits either way.
 template <int LAY>
 __global__ __launch_bounds__(256) void adamw8bit_kernel(
-    long n, float* __restrict__ p, const float* __restrict__ g, uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
+    long n, float* __restrict__ p, float* g, uint8_t* __restrict__ qm, uint8_t* __restrict__ qv,
     float* __restrict__ am, float* __restrict__ av, float b1, float omb1, float b2, float omb2, float eps_c2,
     float step_size, float decay, float gscale, const float* __restrict__ clip, bf16_t* __restrict__ pw,
-    const long* __restrict__ desc, float* __restrict__ m32, float* __restrict__ v32, Adam8Maps maps) {
+    const long* __restrict__ desc, float* __restrict__ m32, float* __restrict__ v32, int zero_grad, Adam8Maps maps) {
 #pragma clang fp contract(off)
   __shared__ float cs[256], cu[256], ts[256], tu[256];
   __shared__ float red[2][4];
@@ -211,6 +211,7 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(
       }
       p[i] = pv[e];
       if (pw) pw[i] = f2bf(pv[e]);
+      if (zero_grad) g[i] = 0.f;
     }
     return;
   }
@@ -289,6 +290,10 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(
         (uint32_t)iv[0] | (uint32_t)iv[1] << 8 | (uint32_t)iv[2] << 16 | (uint32_t)iv[3] << 24;
     *reinterpret_cast<uint32_t*>(qv + o1) =
         (uint32_t)iv[4] | (uint32_t)iv[5] << 8 | (uint32_t)iv[6] << 16 | (uint32_t)iv[7] << 24;
+    if (zero_grad) {  // optimizer.zero_grad folded into the step: the gradient was read above
+      *reinterpret_cast<float4*>(g + o0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(g + o1) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -298,6 +303,7 @@ __global__ __launch_bounds__(256) void adamw8bit_kernel(
       if (pw) pw[i] = f2bf(pv[e]);
       qm[i] = (uint8_t)im[e];
       qv[i] = (uint8_t)iv[e];
+      if (zero_grad) g[i] = 0.f;
     }
   }
   if (t == 0) { am[blk] = nm; av[blk] = nv; }
@@ -397,7 +403,7 @@ void pso_adamw8bit_maps(float* signed_map, float* unsigned_map) {
   adam8_dynamic_map(false, unsigned_map);
 }
 
-static int adam8_launch(long n, int nblk, float* param, void* param_bf16, const float* grad, uint8_t* exp_avg_q,
+static int adam8_launch(long n, int nblk, float* param, void* param_bf16, float* grad, int zero_grad, uint8_t* exp_avg_q,
                         uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v, const long* desc, float* m32,
                         float* v32, float lr, float beta1, float beta2, float eps, float weight_decay, int step,
                         float grad_scale, const float* clip_coef, void* stream) {
@@ -422,7 +428,7 @@ static int adam8_launch(long n, int nblk, float* param, void* param_bf16, const 
   const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2);
 #define PSO_ADAM8_ARGS                                                                                                   \
   n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, beta1, omb1, beta2, omb2, c2 * eps, step_size, decay,     \
-      grad_scale, clip_coef, (bf16_t*)param_bf16, desc, m32, v32, maps
+      grad_scale, clip_coef, (bf16_t*)param_bf16, desc, m32, v32, zero_grad, maps
   if (lay)
     adamw8bit_kernel<1><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
   else
@@ -438,25 +444,44 @@ int pso_adamw8bit_step_bf16(long n, float* param, void* param_bf16, const float*
                 "pso_adamw8bit_step_bf16: bad args");
   PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
                 "pso_adamw8bit_step_bf16: param / grad / param_bf16 need 16-B, the code arrays 8-B alignment");
-  return adam8_launch(n, (int)pso_adamw8bit_blocks(n), param, param_bf16, grad, exp_avg_q, exp_avg_sq_q, absmax_m,
+  return adam8_launch(n, (int)pso_adamw8bit_blocks(n), param, param_bf16, const_cast<float*>(grad), 0, exp_avg_q, exp_avg_sq_q, absmax_m,
                       absmax_v, nullptr, nullptr, nullptr, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
                       clip_coef, stream);
+}
+
+static int adam8_blocks(const char* who, long n, int nblk, const long* desc, float* param, void* param_bf16,
+                        float* grad, int zero_grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m,
+                        float* absmax_v, float* exp_avg_32, float* exp_avg_sq_32, float lr, float beta1, float beta2,
+                        float eps, float weight_decay, int step, float grad_scale, const float* clip_coef,
+                        void* stream) {
+  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0 &&
+                    nblk >= 0 && (nblk == 0 || desc),
+                "%s: bad args", who);
+  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16 | (uintptr_t)exp_avg_32 |
+                  (uintptr_t)exp_avg_sq_32) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
+                "%s: param / grad / param_bf16 / 32-bit state need 16-B, the code arrays 8-B alignment", who);
+  return adam8_launch(n, nblk, param, param_bf16, grad, zero_grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, desc,
+                      exp_avg_32, exp_avg_sq_32, lr, beta1, beta2, eps, weight_decay, step, grad_scale, clip_coef,
+                      stream);
 }
 
 int pso_adamw8bit_step_blocks(long n, int nblk, const long* desc, float* param, void* param_bf16, const float* grad,
                               uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m, float* absmax_v,
                               float* exp_avg_32, float* exp_avg_sq_32, float lr, float beta1, float beta2, float eps,
                               float weight_decay, int step, float grad_scale, const float* clip_coef, void* stream) {
-  PSO_ARG_CHECK(param && grad && exp_avg_q && exp_avg_sq_q && absmax_m && absmax_v && step >= 1 && n > 0 &&
-                    nblk >= 0 && (nblk == 0 || desc),
-                "pso_adamw8bit_step_blocks: bad args");
-  PSO_ARG_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)param_bf16 | (uintptr_t)exp_avg_32 |
-                  (uintptr_t)exp_avg_sq_32) & 15) == 0 && (((uintptr_t)exp_avg_q | (uintptr_t)exp_avg_sq_q) & 7) == 0,
-                "pso_adamw8bit_step_blocks: param / grad / param_bf16 / 32-bit state need 16-B, the code arrays 8-B "
-                "alignment");
-  return adam8_launch(n, nblk, param, param_bf16, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, desc,
-                      exp_avg_32, exp_avg_sq_32, lr, beta1, beta2, eps, weight_decay, step, grad_scale, clip_coef,
-                      stream);
+  return adam8_blocks("pso_adamw8bit_step_blocks", n, nblk, desc, param, param_bf16, const_cast<float*>(grad), 0,
+                      exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, exp_avg_32, exp_avg_sq_32, lr, beta1, beta2, eps,
+                      weight_decay, step, grad_scale, clip_coef, stream);
+}
+
+int pso_adamw8bit_step_blocks_zero_grad(long n, int nblk, const long* desc, float* param, void* param_bf16,
+                                        float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q, float* absmax_m,
+                                        float* absmax_v, float* exp_avg_32, float* exp_avg_sq_32, float lr,
+                                        float beta1, float beta2, float eps, float weight_decay, int step,
+                                        float grad_scale, const float* clip_coef, void* stream) {
+  return adam8_blocks("pso_adamw8bit_step_blocks_zero_grad", n, nblk, desc, param, param_bf16, grad, 1, exp_avg_q,
+                      exp_avg_sq_q, absmax_m, absmax_v, exp_avg_32, exp_avg_sq_32, lr, beta1, beta2, eps,
+                      weight_decay, step, grad_scale, clip_coef, stream);
 }
 
 int pso_adamw8bit_step(long n, float* param, const float* grad, uint8_t* exp_avg_q, uint8_t* exp_avg_sq_q,

@@ -932,25 +932,28 @@ class Adam8State:
         return out
 
 
-def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None, out_bf16=None):
+def adamw8bit_step(param, grad, state, lr, betas, eps, weight_decay, step, grad_scale=1.0, clip=None, out_bf16=None,
+                   zero_grad=False):
     """One 8-bit AdamW step on the flat fp32 param; out_bf16 (same numel, bf16) also receives the updated parameters
-    rounded to bf16 (the working copy), in the same pass."""
+    rounded to bf16 (the working copy), in the same pass.  zero_grad (per-tensor block tables only): the step also
+    zeroes the gradient elements its blocks cover after reading them; returns whether it did."""
     require_cuda(param, grad)
     if out_bf16 is not None:
         assert out_bf16.dtype == torch.bfloat16 and out_bf16.numel() == param.numel() and out_bf16.is_contiguous()
     if state.desc is not None:
-        check(lib().pso_adamw8bit_step_blocks(param.numel(), state.nblk, ptr(state.desc), ptr(param), ptr(out_bf16),
+        fn = "pso_adamw8bit_step_blocks_zero_grad" if zero_grad else "pso_adamw8bit_step_blocks"
+        check(getattr(lib(), fn)(param.numel(), state.nblk, ptr(state.desc), ptr(param), ptr(out_bf16),
                                               ptr(grad), ptr(state.qm), ptr(state.qv), ptr(state.am), ptr(state.av),
                                               ptr(state.m32), ptr(state.v32), float(lr), float(betas[0]),
                                               float(betas[1]), float(eps), float(weight_decay), int(step),
-                                              float(grad_scale), ptr(clip), stream_ptr()),
-              "pso_adamw8bit_step_blocks")
-        return
+                                              float(grad_scale), ptr(clip), stream_ptr()), fn)
+        return zero_grad
     check(lib().pso_adamw8bit_step_bf16(param.numel(), ptr(param), ptr(out_bf16), ptr(grad), ptr(state.qm),
                                         ptr(state.qv), ptr(state.am), ptr(state.av), float(lr), float(betas[0]),
                                         float(betas[1]), float(eps), float(weight_decay), int(step), float(grad_scale),
                                         ptr(clip), stream_ptr()),
           "pso_adamw8bit_step_bf16")
+    return False
 
 
 def zero_(x):

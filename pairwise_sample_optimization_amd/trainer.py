@@ -272,13 +272,17 @@ def lora_optimizer_step(tr):
     cast = True
     if getattr(tr, "adam8", None) is not None:  # train.use_8bit_adam: bitsandbytes AdamW8bit (T:427-435)
         work = _work_copy(tr.unet, master)  # the step also writes the bf16 working copy (no separate cast pass)
-        K.adamw8bit_step(master, grad, tr.adam8, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
-                         grad_scale=scale, clip=tr.clip_buf, out_bf16=work)
+        # with a per-tensor block table the step also zeroes the gradient it reads (the pads between tensors are
+        # zero from allocation and no kernel writes them)
+        zeroed = K.adamw8bit_step(master, grad, tr.adam8, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
+                                  grad_scale=scale, clip=tr.clip_buf, out_bf16=work, zero_grad=True)
         cast = work is None
     else:
+        zeroed = False
         K.adamw_step(master, grad, tr.exp_avg, tr.exp_avg_sq, tr.lr, tr.betas, tr.adam_eps, tr.wd, tr.opt_step,
                      grad_scale=scale, clip=tr.clip_buf)
-    K.zero_(grad)
+    if not zeroed:
+        K.zero_(grad)
     refresh(cast=cast)
 
 

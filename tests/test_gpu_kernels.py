@@ -762,7 +762,13 @@ def test_adamw8bit_per_tensor_vs_restatement(cuda):
             gr[o:o + k] = g_.standard_normal(k).astype(np.float32) * np.float32(10.0 ** (-(i % 5)))
         if step == 3:
             gr[[3, 5001, 7000, 12000]] = [np.nan, np.inf, -np.inf, np.nan]
-        K_.adamw8bit_step(pd, torch.tensor(gr, device=cuda), st, lr, (b1, b2), eps, wd, step, out_bf16=wb)
+        gr[pads] = 7.0  # never read: the pads are no block's
+        gd = torch.tensor(gr, device=cuda)
+        # odd steps also zero the gradient they read (pso_adamw8bit_step_blocks_zero_grad, optimizer.zero_grad T:861)
+        zg = K_.adamw8bit_step(pd, gd, st, lr, (b1, b2), eps, wd, step, out_bf16=wb, zero_grad=step % 2 == 1)
+        gk = gd.cpu().numpy()
+        assert zg == (step % 2 == 1) and np.array_equal(gk[pads], gr[pads])
+        assert (not (gk[~pads] != 0).any()) if zg else np.array_equal(gk, gr, equal_nan=True)
         p = O.adamw8bit_step_tensors(p, gr, segs, ost, lr, b1, b2, eps, wd, step)
     torch.cuda.synchronize()
     pk = pd.cpu().numpy()

@@ -439,6 +439,8 @@ def test_use_8bit_adam_trains_and_checkpoints(cuda, tmp_path):
     torch.cuda.synchronize()
     d8, d32 = u8.lora.master - m0, u32.lora.master - m0
     assert t8.opt_step == 3 and d8.abs().max() > 0
+    # the 8-bit step zeroed the gradient it read (pads included: no kernel writes them)
+    assert u8.lora.grad.abs().max().item() == 0 and u32.lora.grad.abs().max().item() == 0
     cos = (d8 * d32).sum() / (d8.norm() * d32.norm())
     print(f"8-bit vs fp32 AdamW update: cos {cos.item():.4f}, norm ratio {(d8.norm() / d32.norm()).item():.4f}")
     assert cos > 0.95 and 0.8 < (d8.norm() / d32.norm()).item() < 1.25
