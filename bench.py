@@ -70,8 +70,11 @@ def parse():
                          "--mode dmd --num-steps 4 --pairs 1 --gas 1)")
     ap.add_argument("--adam32", action="store_true",
                     help="fp32 AdamW instead of the reference default 8-bit AdamW (config use_8bit_adam = True)")
-    ap.add_argument("--allreduce-bf16", action="store_true",
-                    help="bf16 gradient all-reduce (fp32 accumulation and optimizer; half the xGMI bytes)")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="gradient all-reduce wire dtype (fp32 accumulation and optimizer either way): auto = bf16 for "
+                         "the full-UNet gradient (C3 / C4), fp32 for the LoRA bucket (DESIGN.md §6)")
+    ap.add_argument("--allreduce-bf16", action="store_true", help="alias of --allreduce bf16")
+    ap.add_argument("--cpu-timed", type=int, default=3, help="timed CPU-baseline samples after one warm-up")
     ap.add_argument("--no-extra", action="store_true", help="skip the c3 / lora_bs1 / c5 secondary objects")
     ap.add_argument("--extra-steps", type=int, default=3)
     return ap.parse_args()
@@ -103,7 +106,7 @@ def build(args, dev):
     unet.prepare()
     tr = PSOTrainer(unet, mode=args.mode, num_steps=args.num_steps, gradient_accumulation_steps=args.gas,
                     train_batch_size=args.pairs, num_reward=1, ref_unet=ref_unet,
-                    allreduce_dtype=torch.bfloat16 if getattr(args, "allreduce_bf16", False) else None,
+                    allreduce_dtype=wire_dtype(args),
                     use_8bit_adam=not getattr(args, "adam32", False))  # the reference default (T:427-435)
     g = torch.Generator(device=dev).manual_seed(1000 + int(os.environ.get("RANK", "0")))
     Bp = args.pairs * args.gas  # pairs sampled per epoch per GPU
@@ -113,6 +116,12 @@ def build(args, dev):
     reward = lambda img: torch.rand(img.shape[0], device=dev, generator=g)
     buf = tr.sample_pairs(enc, pooled, tid, h, generator=g, reward_fn=reward)
     return unet, tr, buf, g
+
+
+def wire_dtype(args):
+    if getattr(args, "allreduce_bf16", False):
+        return torch.bfloat16
+    return {"auto": "auto", "fp32": torch.float32, "bf16": torch.bfloat16}[getattr(args, "allreduce", "auto")]
 
 
 def one_step(tr, buf, g, graph=False):
@@ -180,29 +189,65 @@ def roofline(tr, buf, g):
     return out
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args, unet):
     """Oracle (plain torch fp32 CPU restatement, oracle/sdxl_ref.py) on a bounded sample of the same workload: the
-    per-image share of one micro-step at 1024^2 = 1 policy forward + LoRA backward + 1 reference forward."""
+    per-image share of one micro-step at 1024^2 = 1 policy forward + LoRA backward + 1 reference forward (BASELINE.md
+    §3: one warm-up, then >= 3 timed samples; the median is the value, the CPU model and thread count beside it)."""
     from oracle import sdxl_ref
     torch.set_num_threads(args.cpu_threads)
     sd = {k: v.float().cpu() for k, v in unet.state_dict().items()}
     lora = {k: v.float().cpu().requires_grad_(True) for k, v in unet.lora.state_dict_peft().items()}
     h = args.res // 8
-    x = torch.randn(1, 4, h, h)
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(1, 4, h, h, generator=gen)
     t = torch.tensor([999.0])
-    enc = torch.randn(1, 77, 2048)
-    pooled = torch.randn(1, 1280)
+    enc = torch.randn(1, 77, 2048, generator=gen)
+    pooled = torch.randn(1, 1280, generator=gen)
     tid = torch.tensor([[args.res, args.res, 0, 0, args.res, args.res]], dtype=torch.float32)
+
+    def share():
+        out = sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=lora)
+        out.sum().backward()
+        with torch.no_grad():
+            sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=None)
+        for v in lora.values():
+            v.grad = None
+
     t0 = time.perf_counter()
-    out = sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=lora)
-    out.sum().backward()
-    with torch.no_grad():
-        sdxl_ref.unet_forward(sd, x, t, enc, pooled, tid, lora=None)
-    dt = time.perf_counter() - t0
+    share()  # warm-up: allocator, thread pool, first-touch of the fp32 weights
+    warm = time.perf_counter() - t0
+    times = []
+    for _ in range(max(1, args.cpu_timed)):
+        t0 = time.perf_counter()
+        share()
+        times.append(time.perf_counter() - t0)
     del sd, lora
-    return {"value": round(1.0 / dt, 5), "unit": "imgs/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"1 image at {args.res}^2: policy fwd + LoRA bwd + reference fwd, fp32 torch oracle, "
-                      f"{dt:.1f} s"}
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(1.0 / med, 5), "unit": "imgs/s", "cores": args.cpu_threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "warmup_s": round(warm, 2),
+            "timed_s": [round(v, 2) for v in times],
+            "sample": f"1 image at {args.res}^2: policy fwd + LoRA bwd + reference fwd, fp32 torch oracle "
+                      f"(oracle/sdxl_ref.py); 1 warm-up + {len(times)} timed, median {med:.1f} s"}
+
+
+def skipped_ref_prefix_tflop(h):
+    """TFLOP per reference image the paired pass never executes: the adapter-free prefix (conv_in, down_blocks.0's
+    two resnets and downsampler) runs once on the policy images and is duplicated."""
+    m0, m1 = h * h, (h // 2) * (h // 2)
+    c = 320
+    fl = 2 * m0 * c * 4 * 9 + 4 * 2 * m0 * c * c * 9 + 2 * m1 * c * c * 9
+    return fl / 1e12
 
 
 SDXL_FWD_TFLOP_PER_IMG = 6.765   # SURVEY §8d / App. B: one UNet forward at 1024^2
@@ -283,8 +328,10 @@ def sub_config(args, dev, name, steps, warmup=1, **over):
     pair_micro = a.pairs * a.gas * (a.num_steps - 1)
     tf = SURVEY_TFLOP_FULL_UNET if a.full_unet else SURVEY_TFLOP_PER_PAIR_MICRO.get(a.rank)
     if a.res == 1024 and tf:
+        skip = 0.0 if a.full_unet else 2 * pair_micro * skipped_ref_prefix_tflop(a.res // 8)
         out["tflop_per_step"] = round(tf * pair_micro, 2)
-        out["step_mfma_frac"] = round(tf * pair_micro / dt / PEAK_BF16_TFLOPS, 4)
+        out["skipped_ref_prefix_tflop_per_step"] = round(skip, 3)
+        out["step_mfma_frac"] = round((tf * pair_micro - skip) / dt / PEAK_BF16_TFLOPS, 4)
     if not a.no_roofline:
         rf = roofline(tr, buf, g)
         out["roofline"] = {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "avg_launch_us",
@@ -405,7 +452,7 @@ def main():
     torch.manual_seed(rank)
     if os.environ.get("PSO_BENCH_GEMM_VARIANT"):  # A/B knob of the GEMM dispatch (tools/_ab.sh)
         from pairwise_sample_optimization_amd import kernels as K
-        K.lib().pso_gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
+        K.gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
     if os.environ.get("PSO_BENCH_ATTN_VARIANT"):  # A/B knob of the attention kernels
         from pairwise_sample_optimization_amd import kernels as K
         K.lib().pso_attention_set_variant(int(os.environ["PSO_BENCH_ATTN_VARIANT"]))
@@ -454,8 +501,13 @@ def main():
     }
     tf = SURVEY_TFLOP_PER_PAIR_MICRO.get(args.rank) if (args.res == 1024 and not args.full_unet) else None
     if tf:
-        step_tf = tf * args.pairs * args.gas * (args.num_steps - 1)
+        pair_micro = args.pairs * args.gas * (args.num_steps - 1)
+        # executed work: the SURVEY count minus the reference images' adapter-free prefix the paired pass shares
+        skip = 2 * pair_micro * skipped_ref_prefix_tflop(args.res // 8)
+        step_tf = tf * pair_micro - skip
         res["step_mfma_frac"] = round(step_tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)
+        res["step_tflop_executed"] = round(step_tf, 2)
+        res["skipped_ref_prefix_tflop_per_step"] = round(skip, 3)
     if world > 1:
         res["dist"] = dist_report(tr, dev, dt_rank, args.steps)
     if not args.no_roofline:

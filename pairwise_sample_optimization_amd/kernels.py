@@ -88,7 +88,14 @@ def _row_stride(t):
     return t.stride(0)
 
 
-_GEMM_WS = {}  # (M, N, K1, K2) -> pso_gemm_ws_bytes
+_GEMM_WS = {}  # (M, N, K1, K2) -> pso_gemm_ws_bytes of the current dispatch variant
+
+
+def gemm_set_variant(v):
+    """pso_gemm_set_variant (A/B knob of the GEMM dispatch) + a flush of the workspace-size cache: the split-K plan,
+    and so the workspace a product needs, depends on the variant."""
+    lib().pso_gemm_set_variant(int(v))
+    _GEMM_WS.clear()
 
 
 def gemm(a, w, *, bias=None, resid=None, a2=None, w2=None, alpha=1.0, rowbias=None, rows_per_group=1, out=None,
@@ -901,28 +908,88 @@ class Adam8State:
         self.am = torch.zeros(max(self.nblk, 1), dtype=torch.float32, device=device)
         self.av = torch.zeros(max(self.nblk, 1), dtype=torch.float32, device=device)
 
-    def dequant(self):
-        """(m, v) as fp32 over the flat buffer (tests / checkpoints; elements outside every tensor read 0)."""
+    @staticmethod
+    def maps(device):
+        """bitsandbytes' signed (m) / unsigned (v) dynamic code maps, 256 fp32 values each."""
         s = (ctypes.c_float * 256)()
         u = (ctypes.c_float * 256)()
         lib().pso_adamw8bit_maps(s, u)
+        return torch.tensor(list(s), device=device), torch.tensor(list(u), device=device)
+
+    _CHUNK_ROWS = 16384  # block-table rows per vectorised slice (bounds the per-element index tensors to ~32M)
+
+    def _row_chunks(self):
+        """(row ids, element positions, element -> row-in-chunk) per chunk of the block table, on the device."""
         dev = self.qm.device
-        cs = torch.tensor(list(s), device=dev)
-        cu = torch.tensor(list(u), device=dev)
+        d = self.desc
+        for r0 in range(0, self.nblk, self._CHUNK_ROWS):
+            rows = torch.arange(r0, min(r0 + self._CHUNK_ROWS, self.nblk), device=dev)
+            off, ln = d[rows, 0], d[rows, 1]
+            blk = torch.repeat_interleave(torch.arange(rows.numel(), device=dev), ln)
+            first = torch.cumsum(ln, 0) - ln
+            pos = off[blk] + (torch.arange(blk.numel(), device=dev) - first[blk])
+            yield rows, pos, blk
+
+    def dequant(self):
+        """(m, v) as fp32 over the flat buffer (tests / checkpoints; elements outside every tensor read 0).
+        Vectorised over slices of the block table (full-UNet mode has ~1.25M rows)."""
+        dev = self.qm.device
+        cs, cu = self.maps(dev)
         n = self.qm.numel()
         if self.desc is None:
             blk = torch.arange(n, device=dev) // self.BLOCK
             return cs[self.qm.long()] * self.am[blk], cu[self.qv.long()] * self.av[blk]
         m = torch.zeros(n, device=dev)
         v = torch.zeros(n, device=dev)
-        for b, (o, k, so, _) in enumerate(self.rows):
-            if so >= 0:
-                m[o:o + k] = self.m32[so:so + k]
-                v[o:o + k] = self.v32[so:so + k]
-            else:
-                m[o:o + k] = cs[self.qm[o:o + k].long()] * self.am[b]
-                v[o:o + k] = cu[self.qv[o:o + k].long()] * self.av[b]
+        for rows, pos, blk in self._row_chunks():
+            so = self.desc[rows, 2][blk]
+            r32 = so >= 0
+            p8, b8 = pos[~r32], rows[blk[~r32]]
+            m[p8] = cs[self.qm[p8].long()] * self.am[b8]
+            v[p8] = cu[self.qv[p8].long()] * self.av[b8]
+            p32 = pos[r32]
+            if p32.numel():
+                i32 = so[r32] + (p32 - self.desc[rows, 0][blk[r32]])
+                m[p32] = self.m32[i32]
+                v[p32] = self.v32[i32]
         return m, v
+
+    def load_dense(self, m, v):
+        """Quantise fp32 moments m, v over the flat buffer into this state: per block absmax, nearest code of the
+        normalised value (resume from a checkpoint written with another block layout)."""
+        dev = self.qm.device
+        m, v = m.to(dev, torch.float32), v.to(dev, torch.float32)
+        cs, cu = self.maps(dev)
+
+        def nearest(x, cmap):
+            vals, order = torch.sort(cmap)
+            i = torch.clamp(torch.searchsorted(vals, x), 1, vals.numel() - 1)
+            lo, hi = vals[i - 1], vals[i]
+            i = torch.where((x - lo) <= (hi - x), i - 1, i)
+            return order[i].to(torch.uint8)
+
+        if self.desc is None:
+            nb = self.am.numel()
+            pad = nb * self.BLOCK - m.numel()
+            for x, q, a, cmap in ((m, self.qm, self.am, cs), (v, self.qv, self.av, cu)):
+                xb = torch.nn.functional.pad(x, (0, pad)).view(nb, self.BLOCK)
+                a.copy_(xb.abs().amax(1))
+                q.copy_(nearest((xb / a.clamp_min(1e-30)[:, None]).reshape(-1)[:x.numel()], cmap))
+            return
+        for rows, pos, blk in self._row_chunks():
+            so = self.desc[rows, 2][blk]
+            r32 = so >= 0
+            p32 = pos[r32]
+            if p32.numel():
+                i32 = so[r32] + (p32 - self.desc[rows, 0][blk[r32]])
+                self.m32[i32] = m[p32]
+                self.v32[i32] = v[p32]
+            p8, b8 = pos[~r32], rows[blk[~r32]]
+            for x, q, a, cmap in ((m, self.qm, self.am, cs), (v, self.qv, self.av, cu)):
+                xa = x[p8]
+                amax = torch.zeros(self.nblk, device=dev).index_reduce_(0, b8, xa.abs(), "amax", include_self=False)
+                a[rows] = torch.where(self.desc[rows, 2] >= 0, a[rows], amax[rows])
+                q[p8] = nearest(xa / a[b8].clamp_min(1e-30), cmap)
 
     def tensors(self):
         """The state tensors a checkpoint holds (name -> tensor)."""

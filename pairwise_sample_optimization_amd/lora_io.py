@@ -7,10 +7,13 @@
   (and the consumers `T:138`, `evaluate_sdxl_dmd2.py:194`); accepts diffusers (`lora.down/up`) or peft
   (`lora_A/lora_B`) naming, with or without the `unet.` prefix.
 * `save_state(trainer, dir)` / `load_state(trainer, dir)` -- resume (`T:886-890`, `accelerator.save_state`): the
-  LoRA file plus the AdamW moments and step count (`optimizer.safetensors`).
+  LoRA file plus the AdamW moments and step count (`optimizer.safetensors`).  8-bit AdamW checkpoints carry the
+  per-tensor block table (round 4 on); an older checkpoint without one (uniform 2048-element blocks over the flat
+  buffer) is re-quantised into the per-tensor layout on load, with a warning.
 """
 import json
 import os
+import warnings
 
 import torch
 from safetensors.torch import load_file, save_file
@@ -86,12 +89,24 @@ def load_state(trainer, input_dir):
         if "exp_avg_q" not in opt:
             raise KeyError("checkpoint holds fp32 AdamW state; this trainer runs the 8-bit AdamW (use_8bit_adam)")
         mine = a8.tensors()
-        if ("block_table" in mine) != ("block_table" in opt) or (
+        if "block_table" in mine and "block_table" not in opt:
+            # a checkpoint of rounds <= 3: uniform 2048-element blocks over the whole flat buffer.  Its moments are
+            # dequantised in that layout and re-quantised into the per-tensor blocks (lossy only in the code
+            # rounding of the new blocks)
+            warnings.warn("8-bit AdamW checkpoint without a block table (uniform blocks, older format): its moments "
+                          "are re-quantised into the per-tensor block layout")
+            from . import kernels as K
+            old = K.Adam8State(a8.n, a8.qm.device)
+            for k, t in old.tensors().items():
+                t.copy_(opt[k])
+            a8.load_dense(*old.dequant())
+        elif ("block_table" in mine) != ("block_table" in opt) or (
                 "block_table" in opt and not torch.equal(opt["block_table"], mine["block_table"].cpu())):
             raise KeyError("checkpoint's 8-bit AdamW block layout differs from this trainer's parameter tensors")
-        for k, t in mine.items():
-            if k != "block_table":
-                t.copy_(opt[k])
+        else:
+            for k, t in mine.items():
+                if k != "block_table":
+                    t.copy_(opt[k])
     else:
         if "exp_avg" not in opt:
             raise KeyError("checkpoint holds 8-bit AdamW state; this trainer runs fp32 AdamW")

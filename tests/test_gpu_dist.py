@@ -34,6 +34,36 @@ def test_world2_trainer_step_bucketed_overlap(tmp_path):
         assert d["synced_equal_across_ranks"] and d["masters_equal_across_ranks"]
 
 
+def test_world2_full_unet_step_bf16_wire(tmp_path):
+    """The C4 data-parallel step (full-UNet grads, frozen reference UNet, per-tensor 8-bit AdamW, bf16 wire) at world
+    2: bucketed == flat on the same local gradient bit for bit, the overlapped sync within the full-UNet backward's
+    atomic-order noise of it, equal ranks after the optimizer step, and a zero gradient buffer after it
+    (tests/dist_worker_gpu.py --full)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(HERE, "dist_worker_gpu.py"), "--out", str(tmp_path),
+           "--full"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(os.path.join(tmp_path, f"rank{i}.json"))) for i in range(2)]
+    print(res)
+    for d in res:
+        assert d["armed"] and d["buckets"] >= 3
+        assert d["issued_before_finish"] == d["buckets"]
+        assert d["wire"] == "torch.bfloat16" and d["scale"] == 0.5
+        assert d["grad_norm"] > 0
+        assert d["bucketed_equals_flat"]
+        # bf16 wire: an f32-atomic-order difference of the local gradient can flip a bf16 rounding (2^-9 rel)
+        assert d["overlapped_vs_flat_rel"] < 2e-3
+        assert d["synced_equal_across_ranks"] and d["masters_equal_across_ranks"] and d["work_equal_across_ranks"]
+        assert d["weights_moved"]
+        assert d["grad_max_after_step"] == 0.0
+
+
 def test_rccl_world1_bucketed_overlap_on_comm_stream(tmp_path):
     """The product's RCCL path (init_process_group("nccl"), bench.py's backend) on the box's one GPU at world size 1:
     RCCL still runs every collective on its own stream, so this exercises what the gloo tests cannot -- side.join()

@@ -117,11 +117,11 @@ def test_conv_splitk_workspace(cuda, C1, C2, Cout):
     ob2 = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
     assert torch.equal(ob, ob2)
     assert _rel(_nchw(ob), ref + _nchw(res.float())) < 4e-3
-    K_.lib().pso_gemm_set_variant(52)
+    K_.gemm_set_variant(52)
     try:
         on = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
     assert _rel(ob, on) < 4e-3
 
 
@@ -254,7 +254,7 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
     """Every tile configuration on UNet-scale shapes, with and without the grouped LoRA K-tail (3 groups)."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(variant)
+    K_.gemm_set_variant(variant)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + variant)
         a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -276,7 +276,7 @@ def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()  # nothing written past the output
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K,K2,tail_rows,f32", [(2048, 1280, 10240, 0, 0, False), (2048, 1280, 3840, 96, 0, False),
@@ -328,7 +328,7 @@ def test_gemm_8phase(cuda, M, N, K):
     """The 8-phase 256x256 kernel (gemm8p.hip, variant 30): bias epilogue, ragged last row tile, 2..20 K-tiles
     (odd and even K-tile pair counts); nothing is written past the output rows."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(30)
+    K_.gemm_set_variant(30)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + K)
         a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -341,7 +341,7 @@ def test_gemm_8phase(cuda, M, N, K):
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(4096, 3840, 1280, 32, 1280, 2048), (1000, 768, 640, 32, 256, 0),
@@ -351,7 +351,7 @@ def test_gemm_8phase_lora_tail_paired_resid(cuda, M, N, K, K2, group, tail_rows)
     """gemm8p with the LoRA K-tail (grouped per output-column block, or plain), restricted to the first tail_rows rows
     (the policy half of a paired pass), alpha, bias and a residual epilogue; odd / even K-tile counts."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(30)
+    K_.gemm_set_variant(30)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + K + K2)
         a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -374,7 +374,7 @@ def test_gemm_8phase_lora_tail_paired_resid(cuda, M, N, K, K2, group, tail_rows)
         assert _rel(out[tr:], ref[tr:]) < 4e-3 if tr < M else True
         assert (sentinel[M:] == 7.0).all()
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (1000, 640, 640, 32, 640, 0),
@@ -385,7 +385,7 @@ def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
     row tile, odd / even K-tile counts (1..80), the LoRA K-tail grouped per 160-multiple column block or plain,
     restricted to the first tail_rows rows; nothing is written past the output rows."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(38)
+    K_.gemm_set_variant(38)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + K + K2)
         a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -411,7 +411,7 @@ def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
         assert _rel(out, ref) < 4e-3
         assert (sentinel[M:] == 7.0).all()
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (16384, 1280, 1280, 32, 0, 8192),
@@ -425,7 +425,7 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
     main loop -- plain or grouped per 320-multiple column block, restricted to the first tail_rows rows, K2 up to 64;
     nothing is written past the output rows."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(39)
+    K_.gemm_set_variant(39)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + N + K + K2 + 1)
         a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -455,7 +455,7 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
         ref2 = y.bfloat16().float()
         assert _rel(out2, ref2) < 4e-3
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("variant", [0, 31, 45])
@@ -466,7 +466,7 @@ def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
     path (default: the backward on 256 x 320 tiles where they make whole rounds), the 8-phase 256 x 256 backward
     (variant 45) and the 2-phase one (variant 31), against torch fp32 on the same bf16 operands."""
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(variant)
+    K_.gemm_set_variant(variant)
     try:
         g = torch.Generator(device="cuda").manual_seed(M + Fd)
         x = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -495,7 +495,7 @@ def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
         ref = torch.cat([dout * gg * cdf, dout * hh * (cdf + gg * pdf)], 1)[:, idx]
         assert _rel(din, ref) < 6e-3
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("variant", [0, 44])
@@ -519,12 +519,12 @@ def test_conv_8phase_256x320(cuda, variant, B, C, H, W, Cout):
     buf = torch.full((B * H * W * C + 2 * pad,), float("nan"), device=cuda).bfloat16()
     xh = buf[pad:pad + B * H * W * C].view(B, H, W, C)
     xh.copy_(_nhwc(x))
-    K_.lib().pso_gemm_set_variant(variant)
+    K_.gemm_set_variant(variant)
     try:
         out = K_.conv2d(xh, _nhwc(w), bias=bias, rowbias=temb, resid=res)
         kname = K_.lib().pso_last_kernel().decode()
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
     if variant == 44 or (B * H * W // 256) * (Cout // 320) >= 256:
         assert kname == "gemm8p_kernel<0, true, false, false, 320, true>", kname
     assert torch.isfinite(out.float()).all()
@@ -534,7 +534,7 @@ def test_conv_8phase_256x320(cuda, variant, B, C, H, W, Cout):
 @pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
 def test_conv_every_variant_large(cuda, variant):
     from pairwise_sample_optimization_amd import kernels as K_
-    K_.lib().pso_gemm_set_variant(variant)
+    K_.gemm_set_variant(variant)
     try:
         x = torch.randn(4, 320, 64, 64, device=cuda).bfloat16()
         w = (torch.randn(640, 320, 3, 3, device=cuda) / 50).bfloat16()
@@ -542,7 +542,7 @@ def test_conv_every_variant_large(cuda, variant):
         out = K_.conv2d(_nhwc(x), _nhwc(w), out_dtype=torch.float32)
         assert _rel(_nchw(out), ref) < 1e-5
     finally:
-        K_.lib().pso_gemm_set_variant(0)
+        K_.gemm_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 32, 1280), (4096, 96, 1280), (16384, 32, 640), (300, 100, 136),

@@ -183,11 +183,11 @@ def test_attention_fwd_rescale_paths(cuda, variant, case):
 def test_gemm_geglu_fused(cuda, M, dim, variant):
     """GEGLU in the GEMM epilogue (interleaved weight rows) and its backward fused into the dout GEMM, vs torch fp32."""
     from pairwise_sample_optimization_amd import kernels as K
-    K.lib().pso_gemm_set_variant(variant)
+    K.gemm_set_variant(variant)
     try:
         _geglu_case(cuda, M, dim)
     finally:
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
 
 
 def _geglu_case(cuda, M, dim):

@@ -14,7 +14,7 @@ def main():
     dev = torch.device("cuda")
     flush = torch.empty(256 << 20, dtype=torch.bfloat16, device=dev) if os.environ.get("EPI_FLUSH") else None
     for v in [int(x) for x in os.environ.get("GEMM_VARIANTS", "0").split(",")]:
-        K.lib().pso_gemm_set_variant(v)
+        K.gemm_set_variant(v)
         print(f"--- variant {v} flush={flush is not None} ---")
         for M, N, Kd, r in [(16384, 1280, 1280, 32), (8192, 1280, 1280, 32), (65536, 640, 640, 32)]:
             a = torch.randn(M, Kd, device=dev).bfloat16()

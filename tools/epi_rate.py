@@ -18,7 +18,7 @@ def main():
     for _ in range(200):
         x @ x
     Kd = 1280
-    K.lib().pso_gemm_set_variant(30)  # 256 x 256 8-phase wherever it applies
+    K.gemm_set_variant(30)  # 256 x 256 8-phase wherever it applies
     for tiles in (32, 64, 128, 256, 512):
         M, N = 256 * tiles // 4, 1024
         a = torch.randn(M, Kd, device=dev).bfloat16()
@@ -35,7 +35,7 @@ def main():
         print(f"{tiles:4d} tiles ({rounds} round) [{kn}]: loop {out[('plain', 1)]:7.1f} us | plain epilogue "
               f"{(out[('plain', 0)] - out[('plain', 1)]) / rounds:6.1f} us/round | +resid "
               f"{(out[('resid', 0)] - out[('resid', 1)]) / rounds:6.1f} us/round", flush=True)
-    K.lib().pso_gemm_set_variant(0)
+    K.gemm_set_variant(0)
 
 
 if __name__ == "__main__":

@@ -23,12 +23,12 @@ def main():
         w = torch.randn(N, Kd, device=dev).bfloat16()
         res = []
         for name, v, skip in [("2ph", 37, 0), ("8ph", 38, 0), ("8ph-loop", 38, 1)]:
-            K.lib().pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             K.lib().pso_gemm8p_skip_epilogue(skip)
             ms = t_ms(lambda: K.gemm(a, w))
             res.append(f"{name} {2 * M * N * Kd / ms / 1e9:7.1f}")
         K.lib().pso_gemm8p_skip_epilogue(0)
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         print(f"{M}x{N}x{Kd}: " + " | ".join(res) + " TF/s", flush=True)
 
 

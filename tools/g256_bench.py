@@ -26,14 +26,14 @@ def main():
         fl = 2 * M * N * Kd
         res = []
         for v in variants:
-            K.lib().pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             for skip in (0, 1):
                 K.lib().pso_gemm8p_skip_epilogue(skip)
                 ms = t_ms(lambda: K.gemm(a, w))
                 kn = K.lib().pso_last_kernel().decode()
                 res.append(f"v{v}{'-loop' if skip else ''} {fl / ms / 1e9:6.0f}")
             K.lib().pso_gemm8p_skip_epilogue(0)
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         ms = t_ms(lambda: a @ w.t())
         res.append(f"hipBLASLt {fl / ms / 1e9:6.0f}")
         print(f"{M}x{N}x{Kd} [{kn}]: " + " | ".join(res) + " TF/s", flush=True)
@@ -45,14 +45,14 @@ def main():
     r = torch.randn(M, N, device=dev).bfloat16()
     fl = 2 * M * N * Kd
     for v in variants:
-        K.lib().pso_gemm_set_variant(v)
+        K.gemm_set_variant(v)
         res = []
         for name, kw in (("plain", {}), ("bias", dict(bias=b)), ("bias+resid", dict(bias=b, resid=r))):
             ms = t_ms(lambda: K.gemm(a, w, **kw))
             res.append(f"{name} {fl / ms / 1e9:6.0f}")
         print(f"ff.out {M}x{N}x{Kd} v{v} [{K.lib().pso_last_kernel().decode()}]: " + " | ".join(res) + " TF/s",
               flush=True)
-    K.lib().pso_gemm_set_variant(0)
+    K.gemm_set_variant(0)
     # the GEGLU projection (fused epilogue, pre-activation saved for half the rows as in the paired pass)
     for M, N, Kd in [(16384, 10240, 1280), (65536, 5120, 640)]:
         a = torch.randn(M, Kd, device=dev).bfloat16()

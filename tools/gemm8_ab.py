@@ -29,9 +29,9 @@ def main():
         ref = a.float() @ w.float().t()
         res = {m: [] for m in modes + ["auto"]}
         for r in range(3):
-            lib.pso_gemm_set_variant(0)
+            K.gemm_set_variant(0)
             res["auto"].append(t_ms(lambda: K.gemm(a, w)))
-            lib.pso_gemm_set_variant(30)
+            K.gemm_set_variant(30)
             for m in modes:
                 mode(m)
                 res[m].append(t_ms(lambda: K.gemm(a, w)))
@@ -47,7 +47,7 @@ def main():
         w = (torch.randn(2 * F, Kd, device=dev) / Kd ** 0.5).bfloat16()
         b = torch.randn(2 * F, device=dev).bfloat16()
         pre = torch.empty(M // 2, 2 * F, device=dev, dtype=torch.bfloat16)
-        lib.pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         res = {m: [] for m in modes}
         outs = {}
         for r in range(3):
@@ -71,16 +71,16 @@ def main():
         mode(0)
         for r in range(3):
             for v in res:
-                lib.pso_gemm_set_variant(v)
+                K.gemm_set_variant(v)
                 res[v].append(t_ms(lambda: K.gemm_geglu_bwd(dy, wt, pre)))
         for v in res:
-            lib.pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             outs[v] = K.gemm_geglu_bwd(dy, wt, pre).float()
         fl = 2 * M * F * Kd
         print(f"{name:16s} {M}x{F}x{Kd}: " + "  ".join(f"variant {v}: {fl / min(res[v]) / 1e9:6.0f} TF/s" for v in res)
               + f"  maxdiff {(outs[30] - outs[0]).abs().max().item():.1e}", flush=True)
     mode(0)
-    lib.pso_gemm_set_variant(0)
+    K.gemm_set_variant(0)
 
 
 if __name__ == "__main__":

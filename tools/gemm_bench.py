@@ -29,7 +29,7 @@ def main():
     if os.environ.get("GEMM_PREWARM"):  # one silent pass over every shape (first-touch / clock effects)
         run(dev, quiet=True)
     for v in [int(x) for x in os.environ.get("GEMM_VARIANTS", "0").split(",")]:
-        K.lib().pso_gemm_set_variant(v)
+        K.gemm_set_variant(v)
         print(f"--- variant {v} ---")
         run(dev)
 

@@ -31,11 +31,11 @@ def main():
             a = torch.randn(M, Kx, device=dev).bfloat16()
             w = torch.randn(N, Kx, device=dev).bfloat16()
             fl = 2 * M * N * Kx
-            lib.pso_gemm_set_variant(0)
+            K.gemm_set_variant(0)
             t0 = t_ms(lambda: K.gemm(a, w))
             row = [f"K={Kx}: auto {fl / t0 / 1e9:6.0f}"]
             if N % 256 == 0:
-                lib.pso_gemm_set_variant(30)
+                K.gemm_set_variant(30)
                 t1 = t_ms(lambda: K.gemm(a, w))
                 skip(1)
                 t2 = t_ms(lambda: K.gemm(a, w))
@@ -45,7 +45,7 @@ def main():
             t3 = t_ms(lambda: torch.mm(a, wt))
             row.append(f"hipBLASLt {fl / t3 / 1e9:6.0f}")
             res.append("  ".join(row))
-            lib.pso_gemm_set_variant(0)
+            K.gemm_set_variant(0)
             if kk == 1 and M * Kd > 65536 * 1280:
                 break
         print(f"{name} {M}x{N}x{Kd}:")

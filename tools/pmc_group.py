@@ -20,14 +20,14 @@ def main():
            for s in SHAPES}
     plan = []
     for g in GROUPS:
-        K.lib().pso_gemm_set_variant(100 * g)  # g = 0: the automatic group (XCD-chunk aligned)
+        K.gemm_set_variant(100 * g)  # g = 0: the automatic group (XCD-chunk aligned)
         for s in SHAPES:
             a, w = ops[s]
             for _ in range(REPS):
                 K.gemm(a, w)
                 plan.append({"group": g, "shape": s, "algo_bytes": 2 * (s[0] * s[2] + s[1] * s[2] + s[0] * s[1])})
     torch.cuda.synchronize()
-    K.lib().pso_gemm_set_variant(0)
+    K.gemm_set_variant(0)
     print(json.dumps(plan))
 
 

@@ -17,7 +17,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     if os.environ.get("PSO_BENCH_GEMM_VARIANT"):
-        K.lib().pso_gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
+        K.gemm_set_variant(int(os.environ["PSO_BENCH_GEMM_VARIANT"]))
     unet, tr, buf, g = bench.build(args, dev)
     bench.one_step(tr, buf, g)
     torch.cuda.synchronize()

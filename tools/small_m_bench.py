@@ -46,10 +46,10 @@ def geglu_bwd(dev, variants):
         pre = torch.randn(M, 2 * F, device=dev).bfloat16()
         line = f"{M}x{F}x{Kd}".ljust(34)
         for v in variants:
-            K.lib().pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             ms = t_ms(lambda: K.gemm_geglu_bwd(dy, wt, pre))
             line += f"{2 * M * F * Kd / ms / 1e9:8.0f} "
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         print(line, flush=True)
 
 
@@ -101,7 +101,7 @@ def main():
         fl = 2.0 * M * N * Kd + (2.0 * (tr or M) * N * K2 if K2 else 0)
         line = f"{M}x{N}x{Kd}+{K2}/{tr}".ljust(34)
         for v in variants:
-            K.lib().pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             try:
                 out = K.gemm(a, w, **kw)
                 err = ((out.float() - ref).norm() / ref.norm()).item()
@@ -109,7 +109,7 @@ def main():
                 line += f"{fl / ms / 1e9:8.0f}{'!' if err > 1e-2 else ' '}"
             except Exception as e:  # variant not applicable to the shape
                 line += f"{'-':>8} "
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         K.gemm(a, w, **kw)
         kname = K.lib().pso_last_kernel().decode().replace("gemm_bf16_kernel", "2p").replace("gemm8p_kernel", "8p")
         wt = w.t()

@@ -29,14 +29,14 @@ def main():
             ref = a.float().T @ b.float()
         cells = []
         for v in vs:
-            K.lib().pso_gemm_set_variant(v)
+            K.gemm_set_variant(v)
             out = torch.zeros(I, J, device=dev)
             fn = (lambda: K.gemm_tn_geglu(a, b, out)) if kind == "geglu" else (lambda: K.gemm_tn(a, b, out))
             fn()
             rel = ((out - ref).norm() / ref.norm()).item()
             ms = t_ms(fn, it=10)
             cells.append(f"{2.0 * M * I * J / ms / 1e9:6.0f} ({rel:.0e})")
-        K.lib().pso_gemm_set_variant(0)
+        K.gemm_set_variant(0)
         print(f"{M:6d} x {I:5d} x {J:5d} {kind:5s} " + " ".join(f"{c:>14s}" for c in cells), flush=True)
 
 
