@@ -243,7 +243,30 @@ _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
 # "tail": the LoRA up-projection as an e4m3 K-tail; "qkv" (the self-attention q/k/v) is off by default, see
 # enable_fp8_forward
 FP8_KINDS = {"q2", "ff", "tail"}
-_GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"  # ff.proj dW straight into the natural rows (pso_gemm_tn_geglu)
+_GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"
+# diagnostics (tools/c2_window_diag.py): the forward's LoRA-augmented projections rounded as torch/peft round them --
+# bf16(base + bias), bf16(LoRA term), bf16 add, then bf16 residual add -- instead of one rounding of the fused sum
+_TORCH_ROUND = os.environ.get("PSO_TORCH_ROUND", "0") == "1"
+
+
+def _gemm_fwd(a, w, *, a2=None, w2=None, tail_group_n=0, tail_rows=0, bias=None, resid=None, **kw):
+    """K.gemm for the forward's LoRA-augmented projections (PSO_TORCH_ROUND=1: the torch/peft rounding sequence)."""
+    if not _TORCH_ROUND or a2 is None:
+        return K.gemm(a, w, a2=a2, w2=w2, tail_group_n=tail_group_n, tail_rows=tail_rows, bias=bias, resid=resid,
+                      **kw)
+    base = K.gemm(a, w, bias=bias)
+    rows = tail_rows if tail_rows else a.shape[0]
+    N = w.shape[0]
+    if tail_group_n:
+        r = w2.shape[1]
+        lo = torch.cat([K.gemm(a2[:, j * r:(j + 1) * r].contiguous(), w2[j * tail_group_n:(j + 1) * tail_group_n])
+                        for j in range(N // tail_group_n)], 1)
+    else:
+        lo = K.gemm(a2, w2)
+    base[:rows] = (base[:rows].float() + lo.float()).to(BF16)
+    if resid is not None:
+        base = (base.float() + resid.float()).to(BF16)
+    return base  # ff.proj dW straight into the natural rows (pso_gemm_tn_geglu)
 
 
 def _lin_dw(fg, lin, dy, x, rt=None):
@@ -511,7 +534,7 @@ class BasicTransformerBlock(nn.Module):
                                  a2=K.quant_rows_fp8(u_qkv), w2=f8((id(self), "sB_qkv"), L.sB_qkv, ver),
                                  tail_group_n=C, tail_rows=tr)
             else:
-                qkv = K.gemm(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
+                qkv = _gemm_fwd(n1, a1m.w_qkv, a2=u_qkv, w2=L.sB_qkv, tail_group_n=C, tail_rows=tr)
         elif ok8(3 * C, C, "qkv"):
             qkv = K.gemm_fp8(K.quant_rows_fp8(n1), f8((id(self), "qkv"), a1m.w_qkv))
         else:
@@ -522,7 +545,7 @@ class BasicTransformerBlock(nn.Module):
         o1 = a1m.to_out[0]
         if lo:
             u_o1 = K.gemm(pol(a1), L.A_o1)
-            h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1, tail_rows=tr)
+            h1 = _gemm_fwd(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1, tail_rows=tr)
         else:
             h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x)
         # --- cross attention over the 77 text tokens ---
@@ -538,7 +561,7 @@ class BasicTransformerBlock(nn.Module):
                 q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight),
                                 a2=K.quant_rows_fp8(u_q2), w2=f8((id(self), "sB_q2"), L.sB_q2, ver), tail_rows=tr)
             else:
-                q2 = K.gemm(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
+                q2 = _gemm_fwd(n2, a2m.to_q.weight, a2=u_q2, w2=L.sB_q2, tail_rows=tr)
         elif ok8(C, C, "q2"):
             q2 = K.gemm_fp8(K.quant_rows_fp8(n2), f8((id(self), "q2"), a2m.to_q.weight))
         else:
@@ -553,7 +576,7 @@ class BasicTransformerBlock(nn.Module):
         o2 = a2m.to_out[0]
         if lo:
             u_o2 = K.gemm(pol(a2), L.A_o2)
-            h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2, tail_rows=tr)
+            h2 = _gemm_fwd(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2, tail_rows=tr)
         else:
             h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
         # --- GEGLU feed-forward ---
@@ -1244,7 +1267,7 @@ class UNet2DConditionModel(nn.Module):
         if rt.lora_on:
             A, sB = self.lora.kv_stacks[C][:2]  # same block order as grp.W (both follow _attn_modules)
             u = K.gemm(rt.pol(enc), A)
-            kv = K.gemm(enc, grp.W, a2=u, w2=sB, tail_group_n=C, tail_rows=enc.shape[0] // 2 if rt.paired else 0)
+            kv = _gemm_fwd(enc, grp.W, a2=u, w2=sB, tail_group_n=C, tail_rows=enc.shape[0] // 2 if rt.paired else 0)
         else:
             u, kv = None, K.gemm(enc, grp.W)
         rt.kv_cache[C] = (kv, u)
