@@ -15,6 +15,7 @@ Secondary objects on the same JSON line (never the headline value):
               reference UNet, 1 pair per micro-step -- its own warmed-up, timed steps + dominant-kernel roofline;
   "lora_bs1"  the north-star operating point "bs = 1 / GPU": the C2 LoRA step at 1 pair, gas 1 (one micro-step =
               2 policy + 2 reference images in one paired pass);
+  "dmd_lora"  the reference's own DMD2 recipe (config_sdxl_dmd_dpo.py: LoRA r=16, T=3, gas 4) at 1024^2;
   "c5"        BASELINE configs[4] on this GPU: the DreamBooth PSO micro-step (1 instance + 1 negative, r = 16, VAE
               encode in the step), bf16 and with the fp8 forward, and their ratio;
   "dist"      (N > 1) the backend and world size torch.distributed really runs, every rank's ms/step, and the
@@ -530,6 +531,12 @@ def main():
                                     gas=1, full_unet=True),
                          workload="C3: SDXL-DMD2 PSO, 4-step sampler (T=3), full-UNet grads vs a frozen reference UNet, "
                                   "1 pair / micro-step, gas 1, bf16, 1024^2")
+        log("[bench] dmd_lora ...")
+        res["dmd_lora"] = dict(sub_config(args, dev, "dmd_lora", max(1, args.extra_steps - 1), warmup=1, mode="dmd",
+                                          num_steps=4, pairs=1, gas=4, rank=16, full_unet=False),
+                               workload="the reference's own DMD2 recipe (config_sdxl_dmd_dpo.py): LoRA r=16, 4-step "
+                                        "sampler (T=3), 1 pair / micro-step, gas 4 (12 micro-steps = 24 images per "
+                                        "optimizer step, passes of <= 16 images), 8-bit AdamW, bf16, 1024^2")
         log("[bench] c5 ...")
         res["c5"] = c5_metric(dev)
     if rank == 0:

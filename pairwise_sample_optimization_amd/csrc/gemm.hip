@@ -152,6 +152,26 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define PSO_S_WAITCNT(imm) ((void)0)
 #endif
 
+// Wait until at most n K-tiles' worth of this wave's direct-to-LDS loads (P pieces each) are still in flight (n is
+// wave-uniform, 0..3: the STAGES <= 5 rings), then the block barrier; LGKM also retires this wave's LDS reads first.
+template <int P, bool LGKM>
+__device__ __forceinline__ void vm_wait_barrier(int n) {
+  static_assert(3 * P <= 63, "vmcnt field");
+  if (n >= 3) {
+    if (LGKM) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(3 * P) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * P) : "memory");
+  } else if (n == 2) {
+    if (LGKM) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * P) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * P) : "memory");
+  } else if (n == 1) {
+    if (LGKM) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(P) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P) : "memory");
+  } else {
+    if (LGKM) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 // Direct-to-LDS staging (global_load_lds_dwordx4): wave w fills 8-row x 128-B pieces; lane i of a piece lands at
 // byte 16*i of it (row i/8, physical chunk i%8), so the XOR swizzle is applied to the SOURCE chunk: physical chunk p of
 // row R holds logical chunk p ^ (R & 7) -- the same involution swz() applies on the read side.
@@ -403,8 +423,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nt) issue_tile(s, s);
-  if (STAGES == 3 && nt > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PIECES) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  // tile 0 landed; tiles 1 .. STAGES-2 may stay in flight
+  static_assert(STAGES <= 5, "vm_wait_barrier covers rings of up to 5 stages");
+  vm_wait_barrier<PIECES, false>(min(STAGES - 2, nt - 1));
 
   int cur = 0;
   auto mfma_half = [&](const bf16_t* la, const bf16_t* lb, int kk) {
@@ -433,9 +454,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_kernel(GemmArgs g) 
     const bf16_t* lb = stage_ptr(cur) + BM * BK;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) mfma_half(la, lb, kk);
-    // K-tile t+1 must have landed (every wave's pieces) before anyone reads it; tiles beyond stay in flight
-    if (STAGES == 3 && ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // K-tile t+1 must have landed (every wave's pieces) before anyone reads it; tiles t+2 .. stay in flight
+    vm_wait_barrier<PIECES, true>(min(STAGES - 2, nt - t - 2));
     cur = (cur + 1 == STAGES) ? 0 : cur + 1;
   }
   if (half_last) {  // landed: the last loop iteration waited for it (vmcnt(0): nothing was issued beyond it)
@@ -1032,6 +1052,14 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (gv == 20 && n160) return launch<64, 160, 2, 2, 2>(g, st);
   if (gv == 21 && (g.N % 80) == 0 && (g.tail_group_n % 80) == 0) return launch<128, 80, 4, 1, 2>(g, st);
   if (gv == 22 && n160) return launch<64, 160, 2, 2, 3>(g, st);
+  // deeper direct-to-LDS rings for the latency-bound short-K small-M products (4 / 5 stages: 3 / 4 K-tiles in flight)
+  if (gv == 23 && n160) return launch<64, 160, 2, 2, 4>(g, st);
+  if (gv == 24 && n160) return launch<64, 160, 2, 2, 5>(g, st);
+  if (gv == 25 && !bn64_only) return launch<64, 64, 2, 2, 4>(g, st);
+  if (gv == 26 && n160) return launch<128, 160, 2, 2, 4>(g, st);
+  if (gv == 27 && !bn64_only) return launch<64, 128, 2, 2, 4>(g, st);
+  if (gv == 28 && !bn64_only) return launch<128, 128, 2, 4, 4>(g, st);
+  if (gv == 29 && !bn64_only) return launch<64, 64, 2, 2, 5>(g, st);
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).

@@ -243,6 +243,7 @@ _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
 # "tail": the LoRA up-projection as an e4m3 K-tail; "qkv" (the self-attention q/k/v) is off by default, see
 # enable_fp8_forward
 FP8_KINDS = {"q2", "ff", "tail"}
+FP8_MIN_TILES = int(os.environ.get("PSO_FP8_MIN_TILES", "192"))  # see BasicTransformerBlock.fwd (0: no occupancy rule)
 _GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"
 # diagnostics (tools/c2_window_diag.py): the forward's LoRA-augmented projections rounded as torch/peft round them --
 # bf16(base + bias), bf16(LoRA term), bf16 add, then bf16 residual add -- instead of one rounding of the fused sum
@@ -519,8 +520,12 @@ class BasicTransformerBlock(nn.Module):
         n1, st1 = K.layer_norm_fwd(x, self.norm1.weight, self.norm1.bias, 1e-5)
         f8 = rt.fp8  # fp8 forward (config 5): the LayerNorm-fed projections on e4m3 MFMA where the shapes allow
         # (the fp8 LoRA tail reads 16-B rows of the rank-r operands: r % 16 == 0)
+        # ... and only where the e4m3 GEMM's 256 x 256 tiles make at least three quarters of a 256-CU round: below that
+        # the product is latency-bound, not MFMA-bound, and the separate row quantisation makes it slower than the bf16
+        # kernel (C5 at 1 + 1 images: the L2 cross-attention q, 2048 x 1280 -- 40 tiles -- 28 vs 21 us per launch)
         ok8 = lambda n_out, k_in, kind: (f8 is not None and kind in FP8_KINDS and n_out % 256 == 0 and
-                                         k_in % 128 == 0 and (not lo or rt.r % 16 == 0))
+                                         k_in % 128 == 0 and (not lo or rt.r % 16 == 0) and
+                                         ((M + 255) // 256) * (n_out // 256) >= FP8_MIN_TILES)
         ver = rt.lora.version if lo else 0
         if lo:
             u_qkv = K.gemm(pol(n1), L.A_qkv)                                # [Mp, 3r]
@@ -1236,10 +1241,10 @@ class UNet2DConditionModel(nn.Module):
 
     def _fp8_weight(self, key, w, version=0):
         """(e4m3 [N, K], E8M0 [N]) of a weight, quantised per output channel.  Frozen base weights (version 0) are
-        quantised once and cached.  The LoRA sB stacks (version > 0) change at every optimizer step: they are
-        re-quantised on EVERY forward into buffers allocated once, so a hipGraph capture of the epoch records the
-        quantisation kernel and each replay reads the current LoRA weights (a version-keyed cache hit would record
-        nothing and replay the capture-time copies).  The sB stacks are [C, r]-sized: the extra pass is negligible."""
+        quantised once and cached.  The LoRA sB stacks (version > 0) change at every optimizer step: eager forwards
+        re-quantise them once per LoRA version into buffers allocated once; under a hipGraph capture every forward
+        re-quantises, so the capture records the quantisation kernel and each replay reads the current LoRA weights (a
+        version-keyed cache hit would record nothing and replay the capture-time copies)."""
         hit = self._fp8_cache.get(key)
         if version == 0:
             if hit is None:
@@ -1251,7 +1256,10 @@ class UNet2DConditionModel(nn.Module):
             self._fp8_cache[key] = hit
             return hit[1]
         q, e = hit[1]
+        if hit[0] == version and not torch.cuda.is_current_stream_capturing():
+            return hit[1]  # eager: this LoRA version is already quantised (a capture re-records the kernel)
         K.quant_rows_fp8(w, q=q, e=e)
+        self._fp8_cache[key] = (version, hit[1])
         return hit[1]
 
     def kv_text(self, rt, C):

@@ -465,6 +465,110 @@ def test_c2_well_conditioned_window_at_1024(cuda):
     assert abs(loss_off.item() - ref_loss) / abs(ref_loss) > 2 * 1e-3
 
 
+def test_dmd_reference_lora_config_window_at_1024(cuda):
+    """The reference's own DMD2 recipe at full size (config_sdxl_dmd_dpo.py via PSOTrainer.from_config: LoRA r = 16,
+    4-step sampler -> T = 3, 1 pair per micro-step, gradient_accumulation_steps 4 -> a window of 12 micro-steps, 8-bit
+    AdamW, beta 50, eps 0.1; D:313-318, D:777-864) at 1024^2 with two rewards per image and D:420-434's strict-Pareto
+    compare: of the window's 4 pairs one has member 0 dominating, one member 1, one an exact tie and one no dominance
+    -- the last two give pref (0, 0), loss log 2 and no gradient.  The window runs as the trainer runs it (passes of at
+    most 16 images: 8 + 4 micro-steps) against the fp32 oracle; the fp32 step math (latent_dtype float32).
+    Bars: loss within north_star's 1e-3 rel; eps, delta, Delta and the 1,120 LoRA gradients within 1.5x the torch-bf16
+    distance + floor; zero-preference pairs contribute exactly log 2 and nothing to the gradient; LoRA-off rejected."""
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd import kernels as K
+    from pairwise_sample_optimization_amd.config import config_sdxl_dmd_dpo
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNet2DConditionModel, UNetConfig
+    c = config_sdxl_dmd_dpo.get_config()
+    h = 128
+    cfg = UNetConfig.sdxl(h)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(SimpleNamespace(r=c.train.lora_rank, lora_alpha=c.train.lora_rank))
+    unet.lora.init_gaussian(seed=0, b_std=1e-2)  # |delta| / |eps| of a few %: resolved by bf16
+    unet.prepare()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # latent_dtype differs from the config's fp16 (replay modes: their own tests)
+        tr = PSOTrainer.from_config(unet, c, mode="dmd", num_reward=2, latent_dtype=torch.float32)
+    assert (tr.T, tr.P, tr.gas, tr.gas_total, unet.lora.r) == (3, 1, 4, 12, 16) and tr.adam8 is not None
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(3000)
+    Bp = tr.P * tr.gas
+    enc = torch.randn(Bp, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(Bp, 1280, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(1024, 0, cuda).repeat(Bp, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g)
+    # two rewards per image (pickscore, imagereward): dominates / dominated / exact tie / no dominance
+    buf["rewards"] = torch.tensor([[[0.6, 0.7], [0.2, 0.3]], [[0.1, 0.4], [0.5, 0.8]], [[0.5, 0.5], [0.5, 0.5]],
+                                   [[0.9, 0.1], [0.2, 0.6]]], device=cuda)
+    sb = tr.shuffle(buf, generator=g)
+    assert sb.n_micro == 12
+    per_pass = max(1, tr.max_pass_images // (2 * tr.P))
+    passes = [(0, per_pass), (per_pass, sb.n_micro - per_pass)]
+    assert passes == [(0, 8), (8, 4)]
+    st = unet.lora
+    st.grad.zero_()
+    sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
+    leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
+    g16 = {}
+    tot = dict(mine=0.0, ref=0.0, r16=0.0, off=0.0)
+    Dm_all, D32_all, D16_all, d_pairs = [], [], [], []
+    rds, rd16s, eps_rel = [], [], []
+    for s0, cnt in passes:
+        mb = tr.micro_batch(sb, s0, cnt)
+        n = mb.unet_in.shape[0]
+        with torch.no_grad():
+            eps_both, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False, paired_ref=True)
+        pref_k = K.preference(mb.rewards, 1)
+        ws = K.pair_loss_ws(n // 2, mb.x[0].numel(), cuda)
+        _, lp_mine = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[:n].contiguous(), eps_both[n:].contiguous(),
+                                     mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
+        loss_off, _ = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[n:].contiguous(), eps_both[n:].contiguous(),
+                                      mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
+        mine_loss = tr.micro_step(mb).item()
+        g16p = {}
+        ep, er, ref_loss, loss16, lps = _oracle_window(sd, mb, tr, cfg, lora_leaf=leaf, grads16=g16p)
+        for k_, v_ in g16p.items():  # the torch-bf16 window gradient: summed over the passes
+            g16[k_] = v_ if k_ not in g16 else g16[k_] + v_
+        e_pol, e_ref = K.nhwc_to_nchw(eps_both[:n]), K.nhwc_to_nchw(eps_both[n:])
+        eps_rel += [_rel(e_pol, ep), _rel(e_ref, er)]
+        q = lambda t: t.bfloat16().float()
+        d32 = q(ep) - q(er)
+        rds.append(_rel(e_pol - e_ref, d32))
+        rd16s.append(_rel(q(lps.ep16) - q(lps.er16), d32))
+        Dm_all.append((lp_mine[:, 0] - lp_mine[:, 1]).reshape(-1))
+        D32_all.append((lps.lpp - lps.lpr).reshape(-1))
+        D16_all.append((lps.lpp16 - lps.lpr16).reshape(-1))
+        d_pairs.append(pref_k)
+        for k_, v_ in (("mine", mine_loss), ("ref", ref_loss), ("r16", loss16), ("off", loss_off.item())):
+            tot[k_] += v_ * cnt / sb.n_micro  # window loss = mean over its micro-steps
+        # zero-preference micro-steps: loss exactly log 2 (their pairs' pref is (0, 0))
+        zero = (pref_k == 0).all(1)
+        assert zero.any() and (~zero).any()
+    Dm, D32, D16 = torch.cat(Dm_all), torch.cat(D32_all), torch.cat(D16_all)
+    rD, rD16 = _rel(Dm, D32), _rel(D16, D32)
+    rel = abs(tot["mine"] - tot["ref"]) / abs(tot["ref"])
+    rel16 = abs(tot["r16"] - tot["ref"]) / abs(tot["ref"])
+    mine = st.grad_dict_peft()
+    den = sum((v.grad ** 2).sum().item() for v in leaf.values())
+    grel = (sum(((mine[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    rd, rd16 = max(rds), max(rd16s)
+    print(f"DMD2 reference config @1024 (r=16, gas 4, T=3, 24 images in 2 passes): eps rel max {max(eps_rel):.2e}; "
+          f"delta rel mine {rd:.3e} torch-bf16 {rd16:.3e}; Delta fp32 {D32.tolist()} mine {Dm.tolist()} rel mine "
+          f"{rD:.3e} torch-bf16 {rD16:.3e}; window loss mine {tot['mine']:.6f} fp32 {tot['ref']:.6f} torch-bf16 "
+          f"{tot['r16']:.6f} LoRA-off {tot['off']:.6f} rel(mine) {rel:.2e} rel(torch-bf16) {rel16:.2e}; LoRA grad rel "
+          f"mine {grel:.3e} torch-bf16 {grel16:.3e} over {len(leaf)} tensors")
+    assert max(eps_rel) < 3e-2
+    assert rd <= 1.5 * rd16 + 2e-2 and rD <= 1.5 * rD16 + 2e-2
+    assert rel <= 1e-3                                                   # north_star
+    assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
+    assert abs(tot["off"] - math.log(2)) < 1e-6
+    assert abs(tot["off"] - tot["ref"]) / tot["ref"] > 2e-3              # LoRA-off rejected by > 2x the bar
+
+
 @pytest.mark.parametrize("P", [1, 2])
 def test_c3_dmd_full_unet_window_at_1024(cuda, P):
     """C3 (P = 1, one GPU) and C4's per-rank workload (P = 2 pairs per GPU of the 8-GPU global 16, D:777-864): the
