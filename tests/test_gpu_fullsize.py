@@ -465,15 +465,38 @@ def test_c2_well_conditioned_window_at_1024(cuda):
     assert abs(loss_off.item() - ref_loss) / abs(ref_loss) > 2 * 1e-3
 
 
+def _oracle_eps32(cfg, unet, mb, cuda):
+    """fp32 oracle eps (policy with LoRA, reference without) of every image of mb, NCHW (no torch-bf16 pass)."""
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd import kernels as K
+    ocfg = dict(time_proj_dim=cfg.time_proj_dim, addition_time_embed_dim=cfg.addition_time_embed_dim)
+    sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
+    lora = {k: v.float() for k, v in unet.lora.state_dict_peft().items()}
+    x_in = K.nhwc_to_nchw(mb.unet_in).float()
+
+    def fwd(i, lo):
+        return sdxl_ref.unet_forward(sd, x_in[i:i + 1], mb.t[i:i + 1], mb.enc[i:i + 1].float(),
+                                     mb.pooled[i:i + 1].float(), mb.tid[i:i + 1], lora=lo, cfg=ocfg)
+    with torch.no_grad():
+        n = x_in.shape[0]
+        return torch.cat([fwd(i, lora) for i in range(n)]), torch.cat([fwd(i, None) for i in range(n)])
+
+
 def test_dmd_reference_lora_config_window_at_1024(cuda):
     """The reference's own DMD2 recipe at full size (config_sdxl_dmd_dpo.py via PSOTrainer.from_config: LoRA r = 16,
     4-step sampler -> T = 3, 1 pair per micro-step, gradient_accumulation_steps 4 -> a window of 12 micro-steps, 8-bit
-    AdamW, beta 50, eps 0.1; D:313-318, D:777-864) at 1024^2 with two rewards per image and D:420-434's strict-Pareto
-    compare: of the window's 4 pairs one has member 0 dominating, one member 1, one an exact tie and one no dominance
-    -- the last two give pref (0, 0), loss log 2 and no gradient.  The window runs as the trainer runs it (passes of at
-    most 16 images: 8 + 4 micro-steps) against the fp32 oracle; the fp32 step math (latent_dtype float32).
+    AdamW, beta 50, eps 0.1; D:313-318, D:777-864) at 1024^2, run as the trainer runs it (passes of at most 16 images:
+    8 + 4 micro-steps) against the fp32 oracle, with the fp32 step math (latent_dtype float32).
+
+    Two rewards per image and D:420-434's strict-Pareto compare: in micro-steps 4j and 4j+1 member 1 dominates, in 4j+2
+    the rewards tie exactly and in 4j+3 neither dominates -- pref (0, 0): loss log 2, no gradient.  The transitions are
+    built from the fp32 oracle's eps (DP/distilled_inference_with_logprob.py:84-135 means): member 0 at the policy's
+    mean, member 1 at the reference model's, each + 0.25 std of noise -- so every contributing pair's log-ratios differ
+    by ~k^2 |delta|^2 (Delta_0 > 0 > Delta_1) and the window loss leaves log 2 by far more than bf16 moves it.  (On the
+    sampled window both members carry nearly the same Delta and the loss sat 2.5e-4 .. 8.7e-4 from log 2, below what
+    the LoRA-off check can resolve: profiles/r05_dmd_reference_red_1.log, _2.log -- every parity bar passed there.)
     Bars: loss within north_star's 1e-3 rel; eps, delta, Delta and the 1,120 LoRA gradients within 1.5x the torch-bf16
-    distance + floor; zero-preference pairs contribute exactly log 2 and nothing to the gradient; LoRA-off rejected."""
+    distance + floor; LoRA-off (loss = log 2) rejected by > 2x the loss bar."""
     from oracle import sdxl_ref
     from pairwise_sample_optimization_amd import kernels as K
     from pairwise_sample_optimization_amd.config import config_sdxl_dmd_dpo
@@ -499,12 +522,14 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
     enc = torch.randn(Bp, 77, 2048, device=cuda, generator=g).bfloat16()
     pooled = torch.randn(Bp, 1280, device=cuda, generator=g).bfloat16()
     tid = compute_time_ids(1024, 0, cuda).repeat(Bp, 1)
-    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g)
-    # two rewards per image (pickscore, imagereward): dominates / dominated / exact tie / no dominance
-    buf["rewards"] = torch.tensor([[[0.6, 0.7], [0.2, 0.3]], [[0.1, 0.4], [0.5, 0.8]], [[0.5, 0.5], [0.5, 0.5]],
-                                   [[0.9, 0.1], [0.2, 0.6]]], device=cuda)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g,
+                          reward_fn=lambda img: torch.rand(img.shape[0], 2, device=cuda, generator=g))
     sb = tr.shuffle(buf, generator=g)
     assert sb.n_micro == 12
+    # rewards per micro-step (pickscore, imagereward): member 1 dominates / dominates / exact tie / no dominance
+    pattern = torch.tensor([[[0.2, 0.3], [0.6, 0.7]], [[0.1, 0.4], [0.5, 0.8]], [[0.5, 0.5], [0.5, 0.5]],
+                            [[0.9, 0.1], [0.2, 0.6]]], device=cuda)
+    sb.rewards = pattern.repeat(3, 1, 1).contiguous()
     per_pass = max(1, tr.max_pass_images // (2 * tr.P))
     passes = [(0, per_pass), (per_pass, sb.n_micro - per_pass)]
     assert passes == [(0, 8), (8, 4)]
@@ -514,14 +539,28 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
     leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
     g16 = {}
     tot = dict(mine=0.0, ref=0.0, r16=0.0, off=0.0)
-    Dm_all, D32_all, D16_all, d_pairs = [], [], [], []
+    Dm_all, D32_all, D16_all = [], [], []
     rds, rd16s, eps_rel = [], [], []
+    q = lambda t: t.bfloat16().float()
     for s0, cnt in passes:
         mb = tr.micro_batch(sb, s0, cnt)
         n = mb.unet_in.shape[0]
+        # transitions at the fp32 policy (member 0) / reference (member 1) means + 0.25 std of noise
+        ep0, er0 = _oracle_eps32(cfg, unet, mb, cuda)
+        cf = mb.coef
+        c0, c1, c2, c3 = (cf[:, i].view(-1, 1, 1, 1) for i in range(4))
+        xs = mb.x.permute(0, 3, 1, 2)
+        member = (torch.arange(n, device=cuda) % 2).view(-1, 1, 1, 1)
+        eps_mean = torch.where(member == 0, q(ep0), q(er0))
+        xi = torch.randn(xs.shape, device=cuda, generator=torch.Generator(device="cuda").manual_seed(91 + s0))
+        xp = c2 * (xs - c1 * eps_mean) / c0 + 0.25 * c3 * xi
+        mb.x_next = xp.permute(0, 2, 3, 1).contiguous()
+        del ep0, er0
         with torch.no_grad():
             eps_both, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False, paired_ref=True)
         pref_k = K.preference(mb.rewards, 1)
+        zero = (pref_k == 0).all(1)
+        assert zero.any() and (~zero).any() and (pref_k[~zero, 1] == 1).all()
         ws = K.pair_loss_ws(n // 2, mb.x[0].numel(), cuda)
         _, lp_mine = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[:n].contiguous(), eps_both[n:].contiguous(),
                                      mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
@@ -534,19 +573,14 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
             g16[k_] = v_ if k_ not in g16 else g16[k_] + v_
         e_pol, e_ref = K.nhwc_to_nchw(eps_both[:n]), K.nhwc_to_nchw(eps_both[n:])
         eps_rel += [_rel(e_pol, ep), _rel(e_ref, er)]
-        q = lambda t: t.bfloat16().float()
         d32 = q(ep) - q(er)
         rds.append(_rel(e_pol - e_ref, d32))
         rd16s.append(_rel(q(lps.ep16) - q(lps.er16), d32))
         Dm_all.append((lp_mine[:, 0] - lp_mine[:, 1]).reshape(-1))
         D32_all.append((lps.lpp - lps.lpr).reshape(-1))
         D16_all.append((lps.lpp16 - lps.lpr16).reshape(-1))
-        d_pairs.append(pref_k)
         for k_, v_ in (("mine", mine_loss), ("ref", ref_loss), ("r16", loss16), ("off", loss_off.item())):
             tot[k_] += v_ * cnt / sb.n_micro  # window loss = mean over its micro-steps
-        # zero-preference micro-steps: loss exactly log 2 (their pairs' pref is (0, 0))
-        zero = (pref_k == 0).all(1)
-        assert zero.any() and (~zero).any()
     Dm, D32, D16 = torch.cat(Dm_all), torch.cat(D32_all), torch.cat(D16_all)
     rD, rD16 = _rel(Dm, D32), _rel(D16, D32)
     rel = abs(tot["mine"] - tot["ref"]) / abs(tot["ref"])
@@ -556,6 +590,7 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
     grel = (sum(((mine[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
     grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
     rd, rd16 = max(rds), max(rd16s)
+    lo, hi = math.log(1 - tr.clip_eps), math.log(1 + tr.clip_eps)
     print(f"DMD2 reference config @1024 (r=16, gas 4, T=3, 24 images in 2 passes): eps rel max {max(eps_rel):.2e}; "
           f"delta rel mine {rd:.3e} torch-bf16 {rd16:.3e}; Delta fp32 {D32.tolist()} mine {Dm.tolist()} rel mine "
           f"{rD:.3e} torch-bf16 {rD16:.3e}; window loss mine {tot['mine']:.6f} fp32 {tot['ref']:.6f} torch-bf16 "
@@ -563,6 +598,7 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
           f"mine {grel:.3e} torch-bf16 {grel16:.3e} over {len(leaf)} tensors")
     assert max(eps_rel) < 3e-2
     assert rd <= 1.5 * rd16 + 2e-2 and rD <= 1.5 * rD16 + 2e-2
+    assert ((D32 > lo) & (D32 < hi)).all()                                # inside the clip: the gradient flows
     assert rel <= 1e-3                                                   # north_star
     assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
     assert abs(tot["off"] - math.log(2)) < 1e-6
