@@ -27,11 +27,13 @@ def main():
     Bi = int(os.environ.get("ATTN_IMAGES", "8"))
     shapes = [("L1 self", Bi, 10, 4096, 4096), ("L2 self", Bi, 20, 1024, 1024), ("L1 cross", Bi, 10, 4096, 77),
               ("L2 cross", Bi, 20, 1024, 77)]
+    ref = {}
     for v in [int(x) for x in os.environ.get("ATTN_VARIANTS", "0").split(",")]:
         K.lib().pso_attention_set_variant(v)
         print(f"--- variant {v} ---")
         for name, B, H, Sq, Sk in shapes:
             C = H * 64
+            torch.manual_seed(Sq * 7 + Sk)
             q = torch.randn(B, Sq, 3 * C, device=dev).bfloat16()[..., :C]
             k = torch.randn(B, Sk, C, device=dev).bfloat16()
             vv = torch.randn(B, Sk, C, device=dev).bfloat16()
@@ -40,8 +42,16 @@ def main():
             o, lse = K.attention_fwd(q, k, vv, H)
             do = torch.randn(B, Sq, C, device=dev).bfloat16()
             msb = t_ms(lambda: K.attention_bwd(q, k, vv, o, lse, do, H))
+            grads = K.attention_bwd(q, k, vv, o, lse, do, H)
+            same = ""
+            if name in ref:  # every variant must give the bits of the first one (same arithmetic, other schedule)
+                same = " bits " + ("identical" if all(torch.equal(x, y) for x, y in zip(grads, ref[name])) else
+                                   "DIFFER (max %.3g)" % max((x.float() - y.float()).abs().max().item()
+                                                            for x, y in zip(grads, ref[name])))
+            else:
+                ref[name] = [x.clone() for x in grads]
             print(f"{name:10s} B{B} H{H} {Sq}x{Sk}: fwd {ms:7.3f} ms {fl / ms / 1e9:7.1f} TF/s | "
-                  f"bwd {msb:7.3f} ms {2.5 * fl / msb / 1e9:7.1f} TF/s (2.5x fwd flop)")
+                  f"bwd {msb:7.3f} ms {2.5 * fl / msb / 1e9:7.1f} TF/s (2.5x fwd flop){same}", flush=True)
     K.lib().pso_attention_set_variant(0)
 
 
