@@ -330,6 +330,17 @@ __device__ __forceinline__ float rowmax4_asm(float v) {
 
 template <int V> struct ic { static constexpr int value = V; };
 
+// s_waitcnt + s_barrier that leaves the n (<= 3) youngest ring tiles of P LDS-DMA pieces each in flight (n is
+// wave-uniform: the branch is scalar; vmcnt needs an immediate)
+template <int P>
+__device__ __forceinline__ void att_wait_barrier(int n) {
+  static_assert(3 * P <= 63, "vmcnt field");
+  if (n >= 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(3 * P) : "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * P) : "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(P) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // 8 transposed V reads (inline asm, see tr_read_asm) and the wait that makes their registers available: the wait takes
 // the fragments as in/out operands, so no consumer can be scheduled above it
 __device__ __forceinline__ void lds_wait8(s16x4 (&v)[8]) {
@@ -565,13 +576,17 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_fwd2_kernel(AttnArgs a, i
 // PF: the tile's 64 LSE / -delta values are read into registers once, right after the tile's barrier (8 ds_read_b128
 // behind one lgkmcnt wait), instead of one read + wait + scheduling barrier per 16-query subtile -- so nothing pins the
 // S / dP MFMAs of one subtile behind the exp / dS vector work of the previous one
-template <int KJ, int STG, bool PF = false>
+// ONE: one LDS image per operand (Q, dO) in the transposed-read layout (swz_tr), which the row fragment reads
+// (ds_read_b128, 16 rows x 16 B per lane group) also hit conflict-free: half the LDS bytes and DMA traffic per tile,
+// so a deeper ring fits at two workgroups per CU
+template <int KJ, int STG, bool PF = false, bool ONE = false>
 __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_kernel(AttnArgs a, int nkb) {
   constexpr int IMG = ATT_KT * ATT_D;  // elements of one 64 x 64 image
-  constexpr int PIECES = 8;            // 16-B glds per wave per tile (+1 dword piece on waves 0 and 1)
+  constexpr int NIMG = ONE ? 2 : 4;    // images per ring stage
+  constexpr int PIECES = 2 * NIMG;     // 16-B glds per wave per tile (+1 dword piece on waves 0 and 1)
   extern __shared__ __attribute__((aligned(16))) bf16_t att_dyn[];
-  bf16_t* const sbase = att_dyn;                                   // [STG][4][IMG]: Qr, Qt, Or, Ot
-  float* const sLD = reinterpret_cast<float*>(att_dyn + STG * 4 * IMG);  // [STG][2][64]: LSE, delta
+  bf16_t* const sbase = att_dyn;  // [STG][NIMG][IMG]: Qr, Qt, Or, Ot (ONE: Qt, Ot)
+  float* const sLD = reinterpret_cast<float*>(att_dyn + STG * NIMG * IMG);  // [STG][2][64]: LSE, delta
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA destinations (M0) and the LSE / delta resource are scalar
   const int g = lane >> 4, c = lane & 15;
@@ -619,13 +634,20 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
   }
   const int qstep = ATT_KT * (int)a.ldq * 2, ostep = ATT_KT * (int)a.lddo * 2;  // bytes per query tile
   auto issue = [&](int qt, int buf) {
-    bf16_t* img = sbase + buf * 4 * IMG;
+    bf16_t* img = sbase + buf * NIMG * IMG;
     if (wave < 2)  // LSE (wave 0) / delta (wave 1): one dword per lane, issued first so it retires first
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rL, (att_lds_void*)(sLD + (buf * 2 + wave) * 64), 4, lane * 4,
                                                qt * ATT_KT * 4, 0, 0);
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw) {
       const int piece = wave * 2 + pw;
+      if constexpr (ONE) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + piece * 8 * ATT_D), 16, qto[pw], qt * qstep,
+                                                 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rO, (att_lds_void*)(img + IMG + piece * 8 * ATT_D), 16, oto[pw],
+                                                 qt * ostep, 0, 0);
+        continue;
+      }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + piece * 8 * ATT_D), 16, qro[pw], qt * qstep, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + IMG + piece * 8 * ATT_D), 16, qto[pw], qt * qstep,
                                                0, 0);
@@ -663,17 +685,18 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dk[kj][dt] = dv[kj][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (n > 0) issue(qa, 0);
-  if (STG == 3 && n > 1) issue(qa + 1, 1);
+  static_assert(STG >= 2 && STG <= 5, "att_wait_barrier covers rings of up to 5 stages");
+  for (int t = 0; t < STG - 1 && t < n; ++t) issue(qa + t, t);
   for (int i = 0; i < n; ++i) {
-    if (STG == 3 && i + 1 < n) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // tile i landed (this wave's pieces: all but those of the min(STG - 2, n - 1 - i) younger tiles), then every
+    // wave's; the barrier also orders every wave's reads of tile i - 1 before its slot is re-staged below
+    att_wait_barrier<PIECES>(min(STG - 2, n - 1 - i));
     if (i + STG - 1 < n) issue(qa + i + STG - 1, (i + STG - 1) % STG);
     const int buf = i % STG;
-    const bf16_t* sQr = sbase + buf * 4 * IMG;
-    const bf16_t* sQt = sQr + IMG;
-    const bf16_t* sOr = sQr + 2 * IMG;
-    const bf16_t* sOt = sQr + 3 * IMG;
+    const bf16_t* sQt = sbase + buf * NIMG * IMG + (ONE ? 0 : IMG);
+    const bf16_t* sOt = sbase + buf * NIMG * IMG + (ONE ? IMG : 3 * IMG);
+    const bf16_t* sQr = ONE ? sQt : sbase + buf * NIMG * IMG;
+    const bf16_t* sOr = ONE ? sOt : sbase + buf * NIMG * IMG + 2 * IMG;
     const float* sL = sLD + buf * 2 * 64;
     const float* sD = sL + 64;
     const int qbase = (qa + i) * ATT_KT;
@@ -702,8 +725,9 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         bf16x8 qa_[2], oa_[2];
 #pragma unroll
         for (int d2 = 0; d2 < 2; ++d2) {
-          qa_[d2] = *reinterpret_cast<const bf16x8*>(sQr + swz_row(qs * 16 + c, d2 * 4 + g));
-          oa_[d2] = *reinterpret_cast<const bf16x8*>(sOr + swz_row(qs * 16 + c, d2 * 4 + g));
+          const int ro = ONE ? swz_tr(qs * 16 + c, d2 * 4 + g) : swz_row(qs * 16 + c, d2 * 4 + g);
+          qa_[d2] = *reinterpret_cast<const bf16x8*>(sQr + ro);
+          oa_[d2] = *reinterpret_cast<const bf16x8*>(sOr + ro);
         }
         // LSE / delta through inline-asm LDS reads: as plain loads hipcc cannot tell them from the ring's pending
         // LDS-DMA writes and drains the whole ring (vmcnt(0)), prefetch of the next query tile included
@@ -748,16 +772,17 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
         // the wait is tied to the 16 read registers (no scheduling barrier): only the dV / dK MFMAs wait for it, so
         // the compiler may interleave them with the next subtile's independent work
         s16x4 otr[8], qtr[8];
-        const unsigned qtb = (unsigned)(uintptr_t)(const att_lds_void*)sQt;  // sOt = sQt + 16 KB
+        const unsigned qtb = (unsigned)(uintptr_t)(const att_lds_void*)sQt;  // sOt = sQt + 16 KB (ONE: 8 KB)
         auto trd = [&](auto QK_) {
           constexpr int o = decltype(QK_)::value * 4096;  // query rows 32 qk ..
+          constexpr int OT = ONE ? 8192 : 16384;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
             const unsigned ab = qtb + troff[dt];
             qtr[2 * dt] = tr_read_imm<o>(ab);
             qtr[2 * dt + 1] = tr_read_imm<o + 2048>(ab);
-            otr[2 * dt] = tr_read_imm<16384 + o>(ab);
-            otr[2 * dt + 1] = tr_read_imm<16384 + o + 2048>(ab);
+            otr[2 * dt] = tr_read_imm<OT + o>(ab);
+            otr[2 * dt + 1] = tr_read_imm<OT + o + 2048>(ab);
           }
         };
         if (qk == 0) trd(ic<0>{});
@@ -817,17 +842,320 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 }
 
 // ================================================================================================================
+// backward dK/dV, ping-pong form: one workgroup = 8 waves = 256 keys of one (b, h), 32 per wave as in the form above
+// (same arithmetic, same accumulation order: bit-identical dK / dV).  Waves w and w + 4 share a SIMD; the two groups
+// (waves 0-3 / 4-7) share one Q / dO query-tile ring and run one segment apart, every query tile being two segments
+// separated by s_barrier:
+//     A_t (matrix): dV += dO^T P, dK += Q^T dS of tile t - 1 (transposed reads), then S = Q K^T and dP = dO V^T - delta
+//                   of tile t (row reads)                                  -- 64 MFMAs, the LDS reads
+//     B_t (vector): P = exp2(S c - LSE), dS = P dP, packed to bf16        -- 32 exp + ~96 VALU, no MFMA
+// Group 1 takes one extra barrier before its loop and group 0 one after it, so while one wave of a SIMD runs its A
+// segment the other runs its B segment: the exp / dS vector work issues beside the partner's MFMAs instead of in
+// series with its own.  Ring: STG slots of [Q 64 x 64 | dO 64 x 64] (the swz_tr layout serves the row and the
+// transposed reads) + [LSE 64 | -delta 64]; every wave stages one 8-row piece of Q and of dO and the LSE (even waves)
+// or -delta (odd waves) of each tile.  The slot of tile t is last read in group 1's A_{t+1} (global segment 2t + 3),
+// so tile t + STG is issued at global segment 2t + 4 (group 0: at A_{t+2}; group 1: at B_{t+1}) and has 2 STG - 4
+// segments to land before group 0 reads it; each group waits for a tile right before the barrier that opens the
+// segment where it (group 0) or its partner group first reads it.
+// ================================================================================================================
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_b128(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_f32x4(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+// An empty volatile asm that takes a segment's results as in/out operands: they must be computed before it, and it
+// cannot move across the segment's closing s_barrier (volatile asm keeps its order), so the compiler cannot sink a
+// segment's MFMA or VALU work into the next segment (machine sinking otherwise moves the exp / dS block, whose only
+// users are the next segment's MFMAs, behind the barrier, and the two groups' segments stop being complementary)
+template <int A, int B>
+__device__ __forceinline__ void pin_segment(f32x4 (&x)[A][B], f32x4 (&y)[A][B]) {
+  static_assert(A * B == 8 || A * B == 4, "operand count");
+  if constexpr (A * B == 8)
+    asm volatile("" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[0][2]), "+v"(x[0][3]), "+v"(x[1][0]), "+v"(x[1][1]),
+                 "+v"(x[1][2]), "+v"(x[1][3]), "+v"(y[0][0]), "+v"(y[0][1]), "+v"(y[0][2]), "+v"(y[0][3]),
+                 "+v"(y[1][0]), "+v"(y[1][1]), "+v"(y[1][2]), "+v"(y[1][3]));
+}
+template <>
+__device__ __forceinline__ void pin_segment<4, 2>(f32x4 (&x)[4][2], f32x4 (&y)[4][2]) {
+  asm volatile("" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]), "+v"(x[2][0]), "+v"(x[2][1]),
+               "+v"(x[3][0]), "+v"(x[3][1]), "+v"(y[0][0]), "+v"(y[0][1]), "+v"(y[1][0]), "+v"(y[1][1]),
+               "+v"(y[2][0]), "+v"(y[2][1]), "+v"(y[3][0]), "+v"(y[3][1]));
+}
+__device__ __forceinline__ void pp_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// PRIO: the A segment at s_setprio 1.  TR (diagnostic): workgroup 0's waves 0 and 4 record the shader clock before
+// and after every barrier in g_pp_trace (tools/pp_trace.py)
+__device__ unsigned long long g_pp_trace[2][520];
+template <int STG, bool PRIO = false, bool TR = false>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkv_pp_kernel(AttnArgs a, int nkb) {
+  static_assert(STG >= 3 && STG <= 6, "ring depth");
+  constexpr int IMG = ATT_KT * ATT_D;
+  constexpr int P = 3;                      // LDS-DMA loads per wave per tile
+  constexpr unsigned SLOT = 2 * IMG * 2;    // bytes of one slot's Q + dO images
+  constexpr unsigned OIMG = IMG * 2;        // byte offset of the dO image in a slot
+  extern __shared__ __attribute__((aligned(16))) bf16_t att_dyn[];
+  float* const sLD = reinterpret_cast<float*>(att_dyn + STG * 2 * IMG);  // [STG][LSE 64 | -delta 64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;  // (a wave & 1 map, same-phase partners on a SIMD: 1.43 vs 1.18 ms, measured)
+  const int g = lane >> 4, c = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / nkb, kb = bid - bh * nkb;
+  const int h = bh % a.H, b = bh / a.H;
+  const int k0 = kb * 256 + wave * 32;
+
+  const bf16_t* Q = a.q + b * a.sq_b + h * ATT_D;
+  const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
+  const bf16_t* V = a.v + b * a.sv_b + h * ATT_D;
+  const bf16_t* DO = a.dO + b * a.sdo_b + h * ATT_D;
+  const float* LSE = a.lse2 + ((long)b * a.H + h) * a.Sq;  // log2 units
+  const float* DEL = a.delta + ((long)b * a.H + h) * a.Sq;  // -delta
+  const float c2 = a.scale_log2;
+  const int n = (a.Sq + ATT_KT - 1) / ATT_KT;
+
+  // staging (rows past Sq read as zeros through the resources: a padded query has S = 0, p = 1, dP = 0, dS = 0 and
+  // zero Q / dO rows, so it adds nothing -- no mask)
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcT = pch ^ (2 * ((prow >> 1) & 3));
+  const __amdgpu_buffer_rsrc_t rQ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)(((long)(a.Sq - 1) * a.ldq + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rO =
+      __builtin_amdgcn_make_buffer_rsrc((void*)DO, (short)0, (int)(((long)(a.Sq - 1) * a.lddo + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rL =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((wave & 1) ? DEL : LSE), (short)0, a.Sq * 4, 0x00020000);
+  const unsigned qo = (unsigned)((wave * 8 + prow) * (int)a.ldq + lcT * 8) * 2u;
+  const unsigned oo = (unsigned)((wave * 8 + prow) * (int)a.lddo + lcT * 8) * 2u;
+  const int qstep = ATT_KT * (int)a.ldq * 2, ostep = ATT_KT * (int)a.lddo * 2;
+  auto issue = [&](int qt) {
+    const int sl = qt % STG;
+    bf16_t* img = att_dyn + sl * 2 * IMG;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rL, (att_lds_void*)(sLD + sl * 128 + (wave & 1) * 64), 4, lane * 4,
+                                             qt * ATT_KT * 4, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(img + wave * 8 * ATT_D), 16, qo, qt * qstep, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rO, (att_lds_void*)(img + IMG + wave * 8 * ATT_D), 16, oo, qt * ostep, 0,
+                                             0);
+  };
+
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int kj = 0; kj < 2; ++kj) {
+    const int kr = min(k0 + kj * 16 + c, a.Sk - 1);  // clamped keys: computed, never stored
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      kf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(K + (long)kr * a.ldk + ds * 32 + 8 * g));
+      vf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(V + (long)kr * a.ldv + ds * 32 + 8 * g));
+    }
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)(const att_lds_void*)att_dyn;
+  const unsigned ldl = lds0 + STG * SLOT + 16u * g;  // this lane's LSE quad (queries 4g ..) of slot 0
+  // transposed reads (as the form above): one lane offset per 16-column block dt, rows / image / slot are offsets
+  unsigned troff[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int li = lane & 15;
+    const int col = dt * 16 + 4 * (li & 3);
+    troff[dt] = 2u * (unsigned)(swz_tr(4 * g + (li >> 2), col >> 3) + (col & 7));
+  }
+  // row reads: Q[qs * 16 + c][d2 * 32 + 8 g ..] -- the swz_tr XOR of row qs * 16 + c does not depend on qs
+  const unsigned rb0 = 2u * (unsigned)swz_tr(c, g), rb1 = 2u * (unsigned)swz_tr(c, 4 + g);
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int kj = 0; kj < 2; ++kj)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[kj][dt] = dv[kj][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 S[4][2], DP[4][2];   // [qs][kj]: lane holds X[q = qs*16 + 4g + r][k = kj*16 + c]
+  bf16x8 pP[2][2], pS[2][2];  // [qk][kj]: P / dS of the query pairs (qs = 2 qk, 2 qk + 1), packed
+
+  // transposed Q / dO fragments of the tile whose dV / dK the next A segment forms: read at the end of the B segment
+  // (whose wave then waits at the barrier for its partner's longer A segment anyway), so A opens on loaded registers
+  s16x4 qtr[2][8], otr[2][8];
+  auto t_issue_q = [&](int sl, auto QK_) {
+    constexpr int qk = decltype(QK_)::value;
+    const unsigned sb = lds0 + (unsigned)sl * SLOT;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const unsigned ab = sb + troff[dt];
+      qtr[qk][2 * dt] = tr_read_imm<qk * 4096>(ab);
+      qtr[qk][2 * dt + 1] = tr_read_imm<qk * 4096 + 2048>(ab);
+      otr[qk][2 * dt] = tr_read_imm<OIMG + qk * 4096>(ab);
+      otr[qk][2 * dt + 1] = tr_read_imm<OIMG + qk * 4096 + 2048>(ab);
+    }
+  };
+  auto t_issue = [&](int sl) {
+    t_issue_q(sl, ic<0>{});
+    t_issue_q(sl, ic<1>{});
+  };
+  // A: dV / dK of the query pair qk of the previous tile (its fragments landed before the opening barrier)
+  auto m2q = [&](int qk) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 of = cat_frag(otr[qk][2 * dt], otr[qk][2 * dt + 1]);
+      const bf16x8 qf = cat_frag(qtr[qk][2 * dt], qtr[qk][2 * dt + 1]);
+#pragma unroll
+      for (int kj = 0; kj < 2; ++kj) {
+        dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pP[qk][kj], dv[kj][dt], 0, 0, 0);
+        dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, pS[qk][kj], dk[kj][dt], 0, 0, 0);
+      }
+    }
+  };
+  // A: S and dP (onto -delta) of the tile in slot sl (reads of query pair qs + 1 in flight during qs's MFMAs)
+  f32x4 nd[4];
+  bf16x8 fr[2][4];  // [qs parity][qa0 qa1 oa0 oa1]
+  auto m1 = [&](int sl) {
+    const unsigned sb = lds0 + (unsigned)sl * SLOT;
+    const unsigned r0 = sb + rb0, r1 = sb + rb1;
+    const unsigned db = ldl + (unsigned)sl * 512u;  // + 256: -delta
+    nd[0] = lds_f32x4<256>(db);
+    nd[1] = lds_f32x4<256 + 64>(db);
+    nd[2] = lds_f32x4<256 + 128>(db);
+    nd[3] = lds_f32x4<256 + 192>(db);
+    auto rd = [&](auto QS_) {
+      constexpr int qs = decltype(QS_)::value;
+      fr[qs & 1][0] = lds_b128<qs * 2048>(r0);
+      fr[qs & 1][1] = lds_b128<qs * 2048>(r1);
+      fr[qs & 1][2] = lds_b128<OIMG + qs * 2048>(r0);
+      fr[qs & 1][3] = lds_b128<OIMG + qs * 2048>(r1);
+    };
+    auto mm = [&](auto QS_) {
+      constexpr int qs = decltype(QS_)::value;
+      bf16x8(&f)[4] = fr[qs & 1];
+      if (qs == 0)  // the 4 delta reads and qs 0's 4 fragments; qs 1's 4 stay in flight
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(nd[0]), "+v"(nd[1]),
+                     "+v"(nd[2]), "+v"(nd[3]));
+      else if (qs < 3)
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+#pragma unroll
+      for (int kj = 0; kj < 2; ++kj) {
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = nd[qs];
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], kf[kj][0], sacc, 0, 0, 0);
+        S[qs][kj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[1], kf[kj][1], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[2], vf[kj][0], pacc, 0, 0, 0);
+        DP[qs][kj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[3], vf[kj][1], pacc, 0, 0, 0);
+      }
+    };
+    rd(ic<0>{});
+    rd(ic<1>{});
+    mm(ic<0>{});
+    rd(ic<2>{});
+    mm(ic<1>{});
+    rd(ic<3>{});
+    mm(ic<2>{});
+    mm(ic<3>{});
+    pin_segment(S, DP);
+  };
+  // B: P and dS of the tile in slot sl, packed
+  auto vseg = [&](int sl) {
+    const unsigned lb = ldl + (unsigned)sl * 512u;
+    f32x4 lq[4];
+    lq[0] = lds_f32x4<0>(lb);
+    lq[1] = lds_f32x4<64>(lb);
+    lq[2] = lds_f32x4<128>(lb);
+    lq[3] = lds_f32x4<192>(lb);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lq[0]), "+v"(lq[1]), "+v"(lq[2]), "+v"(lq[3]));
+#pragma unroll
+    for (int qk = 0; qk < 2; ++qk)
+#pragma unroll
+      for (int kj = 0; kj < 2; ++kj) {
+        f32x4 pv[2], dsv[2];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int qs = 2 * qk + qh;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = fast_exp2(fmaf(S[qs][kj][r], c2, -lq[qs][r]));
+            pv[qh][r] = pr;
+            dsv[qh][r] = pr * DP[qs][kj][r];
+          }
+        }
+        pP[qk][kj] = pack_p(pv[0], pv[1]);
+        pS[qk][kj] = pack_p(dsv[0], dsv[1]);
+      }
+    asm volatile("" : "+v"(pP[0][0]), "+v"(pP[0][1]), "+v"(pP[1][0]), "+v"(pP[1][1]), "+v"(pS[0][0]), "+v"(pS[0][1]),
+                 "+v"(pS[1][0]), "+v"(pS[1][1]));
+  };
+
+  const bool trw = TR && blockIdx.x == 0 && (wave & 3) == 0 && lane == 0;
+  int trn = 0;
+  auto trace = [&]() {
+    if (TR) {
+      const unsigned long long tc = __builtin_amdgcn_s_memtime();
+      if (trw && trn < 520) g_pp_trace[grp][trn] = tc;
+      ++trn;
+    }
+  };
+  for (int t = 0; t < STG && t < n; ++t) issue(t);
+  if (grp) att_wait_barrier<P>(min(n - 1, STG - 1));  // group 1's extra barrier: it runs one segment behind
+  for (int t = 0;; ++t) {
+    trace();  // (TR: end of the previous segment's work, before its barrier wait)
+    // barrier opening A_t: group 0 first reads tile t in it
+    if (!grp && t < n) att_wait_barrier<P>(min(n - 1, max(STG - 1, t + STG - 3)) - t);
+    else pp_bar();
+    trace();
+    if (!grp && t >= 2 && t + STG - 2 < n) issue(t + STG - 2);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    if (t > 0) {
+      m2q(0);
+      m2q(1);
+      pin_segment(dv, dk);
+    }
+    if (t == n) break;
+    m1(t % STG);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    // barrier opening B_t: group 1's partner (group 0) reads tile t + 1 right after it
+    trace();
+    if (grp) att_wait_barrier<P>(t + 1 < n ? min(n - 1, max(STG - 1, t + STG - 2)) - (t + 1) : 0);
+    else pp_bar();
+    trace();
+    if (grp && t >= 1 && t + STG - 1 < n) issue(t + STG - 1);
+    vseg(t % STG);
+    t_issue(t % STG);
+  }
+  if (!grp) pp_bar();  // group 0's extra barrier: every wave takes 2 n + 2
+
+  const float sc = a.scale_log2 * 0.69314718055994531f;
+#pragma unroll
+  for (int kj = 0; kj < 2; ++kj) {
+    const int kr = k0 + kj * 16 + c;
+    if (kr >= a.Sk) continue;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = h * ATT_D + dt * 16 + 4 * g;
+      *reinterpret_cast<uint2*>(a.dk + b * a.sdk_b + (long)kr * a.lddk + d) =
+          make_uint2(pack2bf(dk[kj][dt][0] * sc, dk[kj][dt][1] * sc), pack2bf(dk[kj][dt][2] * sc, dk[kj][dt][3] * sc));
+      *reinterpret_cast<uint2*>(a.dv + b * a.sdv_b + (long)kr * a.lddv + d) =
+          make_uint2(pack2bf(dv[kj][dt][0], dv[kj][dt][1]), pack2bf(dv[kj][dt][2], dv[kj][dt][3]));
+    }
+  }
+}
+
+// ================================================================================================================
 // backward dQ: forward structure (128 queries per workgroup, S^T = K.Q^T lane-local per query), K/V tiles through LDS;
 // also forms delta[b][h][q] = sum_d dO * O for its queries (stored for the dK/dV kernel launched after it)
 //   dP^T = V . dO^T ; dS^T = P^T * (dP^T - delta) ; dQ^T[d][q] += K^T . dS^T  (K^T via transposed reads)
 // ================================================================================================================
+// ONE: the K row reads come from the transposed-read image (swz_tr serves both reads conflict-free), so a stage holds
+// two images instead of three
+template <int STG = 3, bool ONE = false>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  // K/V tiles arrive by LDS-DMA through a 3-stage ring (two tiles in flight behind a counted vmcnt, one barrier per
-  // tile) as three images per stage: K row image, K transposed-read image, V row image (source-side swizzles).
-  constexpr int STG = 3;
-  constexpr int PIECES = 6;  // glds per wave per tile: 2 pieces x 3 images
+  // K/V tiles arrive by LDS-DMA through a STG-stage ring (STG - 1 tiles in flight behind a counted vmcnt, one barrier
+  // per tile) as three images per stage: K row image, K transposed-read image, V row image (source-side swizzles).
+  static_assert(STG == 3 || STG == 4, "ring depth");
+  constexpr int NIMG = ONE ? 2 : 3;
+  constexpr int PIECES = 2 * NIMG;  // glds per wave per tile: 2 pieces per image
   constexpr int IMG = ATT_KT * ATT_D;
-  __shared__ __attribute__((aligned(16))) bf16_t sRing[STG][3][IMG];
+  __shared__ __attribute__((aligned(16))) bf16_t sRing[STG][NIMG][IMG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: LDS-DMA destinations (M0) are scalar
   const int g = lane >> 4, c = lane & 15;
@@ -902,27 +1230,26 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw) {
       const int piece = wave * 2 + pw;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, kro[pw],
-                                               kt * kstep, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][1] + piece * 8 * ATT_D), 16, kto[pw],
-                                               kt * kstep, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (att_lds_void*)(sRing[buf][2] + piece * 8 * ATT_D), 16, vro[pw],
-                                               kt * vstep, 0, 0);
+      if constexpr (!ONE)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, kro[pw],
+                                                 kt * kstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (att_lds_void*)(sRing[buf][NIMG - 2] + piece * 8 * ATT_D), 16,
+                                               kto[pw], kt * kstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (att_lds_void*)(sRing[buf][NIMG - 1] + piece * 8 * ATT_D), 16,
+                                               vro[pw], kt * vstep, 0, 0);
     }
   };
-  issue(0, 0);
-  if (nkt > 1) issue(1, 1);
+  for (int t = 0; t < STG - 1 && t < nkt; ++t) issue(t, t);
   // the tile loop unrolled by the ring depth: every LDS fragment address is a lane base + an immediate
   auto tile = [&](auto BUF_, int kt) {
     constexpr int buf = decltype(BUF_)::value;
     // tile kt landed (all but this wave's PIECES youngest), then every wave's; the barrier also orders every wave's
     // reads of tile kt-1 before its buffer is re-staged below
-    if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + 2 < nkt) issue(kt + 2, (buf + 2) % STG);
-    const bf16_t* sKr = sRing[buf][0];
-    const bf16_t* sKt = sRing[buf][1];
-    const bf16_t* sVr = sRing[buf][2];
+    att_wait_barrier<PIECES>(min(STG - 2, nkt - 1 - kt));
+    if (kt + STG - 1 < nkt) issue(kt + STG - 1, (buf + STG - 1) % STG);
+    const bf16_t* sKt = sRing[buf][NIMG - 2];
+    const bf16_t* sKr = ONE ? sKt : sRing[buf][0];
+    const bf16_t* sVr = sRing[buf][NIMG - 1];
     const int kbase = kt * ATT_KT;
     // the tile body in two straight-line forms: the key mask of a partial last tile is decided once per tile, not
     // per (key block, query block) -- a branch there splits the body into 16 blocks the scheduler cannot interleave
@@ -934,7 +1261,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
       bf16x8 kf[2], vf[2];
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
-        kf[ds] = *reinterpret_cast<const bf16x8*>(sKr + swz_row(kj * 16 + c, ds * 4 + g));
+        kf[ds] = *reinterpret_cast<const bf16x8*>(sKr + (ONE ? swz_tr(kj * 16 + c, ds * 4 + g) : swz_row(kj * 16 + c, ds * 4 + g)));
         vf[ds] = *reinterpret_cast<const bf16x8*>(sVr + swz_row(kj * 16 + c, ds * 4 + g));
       }
 #pragma unroll
@@ -993,6 +1320,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_dq_kernel(AttnArgs a)
     tile(ic<0>{}, kt);
     if (kt + 1 < nkt) tile(ic<1>{}, kt + 1);
     if (kt + 2 < nkt) tile(ic<2>{}, kt + 2);
+    if constexpr (STG > 3)
+      if (kt + 3 < nkt) tile(ic<3>{}, kt + 3);
   }
   const float sc = a.scale_log2 * 0.69314718055994531f;
   bf16_t* DQ = a.dq + b * a.sdq_b + h * ATT_D;
@@ -1042,16 +1371,23 @@ static int cross_qsplit(int B, int H, int Sq, int Sk) {
 
 static int g_attn_fwd_variant = 0;
 static bool g_attn_vsum = false;
-static int g_attn_bwd_variant = 0;  // benchmark knob: 0 auto, 2 / 4 = keys per wave / 16  // benchmark knob: 0 auto, 2 / 4 = queries per wave / 16
+static int g_attn_bwd_variant = 0;  // benchmark knob (the tens digit of pso_attention_set_variant): see pso_attention_bwd
+static bool g_attn_pp_trace = false;  // the ping-pong dK/dV form records segment clocks (diagnostic)
 
 static bool a16(const void* p, long ld) { return (((uintptr_t)p) & 15) == 0 && (ld % 8) == 0; }
 
 extern "C" {
 
+// diagnostic: the segment-start clocks of the last traced ping-pong dK/dV launch (2 x 520, group-major)
+int pso_attn_pp_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_trace), sizeof(g_pp_trace)) == hipSuccess ? 0 : 1;
+}
+
 void pso_attention_set_variant(int v) {
   g_attn_fwd_variant = v % 10;
   g_attn_bwd_variant = (v / 10) % 10;
-  g_attn_vsum = v >= 100;  // 100+: row sums on the VALU (A/B knob)
+  g_attn_vsum = (v / 100) % 10 == 1;  // 100+: row sums on the VALU (A/B knob)
+  g_attn_pp_trace = (v / 1000) % 10 == 1;
 }
 
 int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
@@ -1135,7 +1471,14 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   a.nbatch = B;
   // dQ first: it forms delta = rowsum(dO * O) for its own queries and stores it for the dK/dV sweep (no separate
   // delta pre-pass launch)
-  attn_bwd_dq_kernel<<<dim3(cdiv(Sq, 128), H, B), ATT_THREADS, 0, st>>>(a);
+  // one LDS image per operand (ONE) by default: bit-identical to the two-image form (bwd variant 3, A/B knob) and
+  // 3-5 % faster on the self-attention shapes (L1 1.113 vs 1.157 ms, L2 0.168 vs 0.177 ms, medians of 4 alternated
+  // runs, profiles/r05_attn_bwd_ab.log); 5 / 6 = ONE with rings of 3 / 4 (no faster)
+  const int bv = g_attn_bwd_variant;
+  const dim3 gq(cdiv(Sq, 128), H, B);
+  if (bv == 3 || bv == 1) attn_bwd_dq_kernel<3, false><<<gq, ATT_THREADS, 0, st>>>(a);
+  else if (bv == 6) attn_bwd_dq_kernel<4, true><<<gq, ATT_THREADS, 0, st>>>(a);
+  else attn_bwd_dq_kernel<3, true><<<gq, ATT_THREADS, 0, st>>>(a);
   // keys per wave: 32 (2 x 16, 128 keys per workgroup, 2 workgroups per CU); 64 on request (benchmark knob)
   const int nkb4 = cdiv(Sk, 256);
   const bool kj4 = g_attn_bwd_variant == 4;  // measured slower on every UNet shape (1 wave/SIMD, AGPR spills)
@@ -1148,10 +1491,44 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
       attr4 = true;
     }
     attn_bwd_dkv_kernel<4, 3><<<nkb4 * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb4);
+  } else if ((bv == 8 || bv == 9) && qsplit == 1) {
+    // ping-pong form (A/B knob, bit-identical; measured no faster: DESIGN §9): 8 waves, 256 keys per workgroup;
+    // 9: A segments at raised priority; the 1000s digit of the variant traces segment clocks
+    constexpr int PST = 4;
+    const size_t shm = PST * (2 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_pp_kernel<PST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm);
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_pp_kernel<PST, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_pp_kernel<PST, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      attr8 = true;
+    }
+    const dim3 gk(nkb4 * H * B);
+    if (g_attn_pp_trace) attn_bwd_dkv_pp_kernel<PST, false, true><<<gk, 512, shm, st>>>(a, nkb4);
+    else if (bv == 9) attn_bwd_dkv_pp_kernel<PST, true><<<gk, 512, shm, st>>>(a, nkb4);
+    else attn_bwd_dkv_pp_kernel<PST><<<gk, 512, shm, st>>>(a, nkb4);
+  } else if (bv != 1 && bv != 3) {  // ONE: Q / dO once per stage (swz_tr image for row and transposed reads)
+    const int stg = bv == 5 ? 3 : (bv == 6 ? 4 : 2);
+    const size_t shm = stg * (2 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    static bool attr1 = false;
+    if (!attr1) {
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<2, 3, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * shm / stg));
+      (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<2, 4, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * shm / stg));
+      attr1 = true;
+    }
+    const dim3 gk(nkb * qsplit * H * B);
+    if (stg == 3) attn_bwd_dkv_kernel<2, 3, true, true><<<gk, ATT_THREADS, shm, st>>>(a, nkb);
+    else if (stg == 4) attn_bwd_dkv_kernel<2, 4, true, true><<<gk, ATT_THREADS, shm, st>>>(a, nkb);
+    else attn_bwd_dkv_kernel<2, 2, true, true><<<gk, ATT_THREADS, shm, st>>>(a, nkb);
   } else if (g_attn_bwd_variant == 1) {  // per-subtile LSE / delta reads (the round-3 form, A/B knob)
     const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
     attn_bwd_dkv_kernel<2, 2><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
-  } else {  // tile-level LSE / delta prefetch: L1 self-attention backward 1.156-1.179 vs 1.188-1.233 ms
+  } else {  // two images per operand (variant 3): tile-level LSE / delta prefetch
     const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
     attn_bwd_dkv_kernel<2, 2, true><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
   }

@@ -85,6 +85,43 @@ def test_attention_fwd_bit_deterministic_eager_and_graph(cuda, shape, spike):
     assert ((mine - ref).norm() / ref.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(4, 10, 4096, 4096), (8, 20, 1024, 1024), (3, 10, 1000, 1000), (4, 10, 4096, 77),
+                                   (2, 20, 1000, 77)])
+@pytest.mark.parametrize("spike", [False, True])
+def test_attention_bwd_forms_bit_identical(cuda, shape, spike):
+    """The dK/dV / dQ forms give the same bits: the default one-image LDS ring (Q / dO staged once in the transposed-read
+    layout), the two-image ring (bwd variant 3) and the 8-wave ping-pong dK/dV (variant 8, and 9 at raised priority;
+    self-attention only -- cross-attention keeps the query-split form), each reproducible run to run, on
+    ragged (1000-token) and spiked inputs; and the default matches an fp32 autograd reference."""
+    from pairwise_sample_optimization_amd import kernels as K
+    B, H, Sq, Sk = shape
+    q, k, v = _attn_inputs(cuda, B, H, Sq, Sk, seed=17, spike=spike)
+    o, lse = K.attention_fwd(q, k, v, H)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    do = torch.randn(B, Sq, H * 64, device=cuda, generator=g).bfloat16()
+    grads = {}
+    for variant in (0, 30, 80, 90):
+        def go():
+            a = [x.clone() for x in K.attention_bwd(q, k, v, o, lse, do, H)]
+            b = K.attention_bwd(q, k, v, o, lse, do, H)
+            return a, b
+        a, b = _run_variant(K, variant, go)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), f"bwd variant {variant}: not reproducible"
+        grads[variant] = a
+    for variant in (30, 80, 90):
+        for name, x, y in zip(("dq", "dk", "dv"), grads[variant], grads[0]):
+            assert torch.equal(x, y), f"bwd variant {variant}: {name} differs from the default form"
+    # fp32 reference on two heads
+    qf, kf, vf, dof = (t.float().view(B, -1, H, 64)[:, :, :2].transpose(1, 2).detach().requires_grad_(True)
+                       for t in (q, k, v, do))
+    ref = torch.softmax(qf @ kf.transpose(-1, -2) / 8.0, -1) @ vf
+    ref.backward(dof)
+    for name, mine, r in zip(("dq", "dk", "dv"), grads[0], (qf.grad, kf.grad, vf.grad)):
+        m = mine.float().view(B, -1, H, 64)[:, :, :2].transpose(1, 2)
+        assert ((m - r).norm() / r.norm()).item() < 2e-2, name
+
+
 def test_unet_paired_forward_graph_bit_exact_at_1024(cuda):
     """The paired UNet forward (2 policy + 2 reference images at 1024^2, LoRA on the policy rows) replayed from a
     hipGraph gives the eager forward's bits, for both attention row-max forms."""

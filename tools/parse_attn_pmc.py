@@ -34,8 +34,8 @@ def main():
         for k, cs in load(p).items():
             for cn, vs in cs.items():
                 agg[k][cn] = sum(vs) / len(vs)
-    print("| kernel | grid | MFMA | VALU | TRANS | VALU/MFMA | MFMA busy | issue-stall | wait |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    print("| kernel | grid | MFMA | VALU | TRANS | VALU/MFMA | MFMA busy | issue-stall | wait | LDS conflict/LDS active | LDS wait |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|")
     for (name, grid), c in sorted(agg.items()):
         if "attn" not in name or "SQ_INSTS_MFMA" not in c:
             continue
@@ -43,7 +43,9 @@ def main():
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / 1024 / max(c.get("GRBM_GUI_ACTIVE", 1) / 8, 1)
         wc = max(c.get("SQ_WAVE_CYCLES", 1), 1)
         print(f"| `{name}` | {grid} | {mf / 1e6:.1f}M | {va / 1e6:.1f}M | {tr / 1e6:.1f}M | {va / max(mf, 1):.2f} | "
-              f"{busy:.2f} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | {c.get('SQ_WAIT_ANY', 0) / wc:.2f} |")
+              f"{busy:.2f} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | {c.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
+              f"{c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_ACTIVE_INST_LDS', 1), 1):.2f} | "
+              f"{c.get('SQ_WAIT_INST_LDS', 0) / wc:.2f} |")
 
 
 if __name__ == "__main__":
