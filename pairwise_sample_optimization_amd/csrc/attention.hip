@@ -897,7 +897,7 @@ __device__ __forceinline__ void pp_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\
 __device__ unsigned long long g_pp_trace[2][520];
 template <int STG, bool PRIO = false, bool TR = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkv_pp_kernel(AttnArgs a, int nkb) {
-  static_assert(STG >= 3 && STG <= 6, "ring depth");
+  static_assert(STG == 3 || STG == 4, "ring depth: the counted waits encode at most 3 younger tiles");
   constexpr int IMG = ATT_KT * ATT_D;
   constexpr int P = 3;                      // LDS-DMA loads per wave per tile
   constexpr unsigned SLOT = 2 * IMG * 2;    // bytes of one slot's Q + dO images
