@@ -18,7 +18,11 @@ there (sqrt(sum_i (dL/dDelta_i)^2 err_i^2), ~8e-3 rel: beta = 50 times pair diff
 to exactness of the loss stage on its own log-probs and training-pass == inference-pass bits.  Every window is built so the policy-vs-reference difference is resolved by bf16 (|delta| / |eps| of a
 few %), and each test checks that its bars REJECT the path that loses that difference (Delta = 0, loss = log 2).
 The oracle runs image by image (the pair loss couples images only through the scalar log-probs), so its fp32
-autograd graph holds one 1024^2 image at a time."""
+autograd graph holds one 1024^2 image at a time.  By default the torch convolutions (MIOpen) differ call to call, and
+so does every bar built from one torch-bf16 draw: the C2 window's 2x LoRA-off margin passed on one box and failed on
+the next (`profiles/r05_c2_window_lora_off_red.log`), so that test runs its yardstick forwards on MIOpen's
+deterministic algorithms (conftest `deterministic_yardstick`; 1.2 s per 1024^2 forward instead of 0.04-0.08 s, so the
+tests whose margins do not hinge on one draw keep the default)."""
 import math
 from types import SimpleNamespace
 
@@ -109,6 +113,11 @@ def _oracle_window(unet_sd, mb, tr, cfg, lora_leaf=None, param_leaf=None, ref_sd
     loss16 = losses16.mean().item()
     lps = SimpleNamespace(lpp=lpp.detach(), lpr=lpr.detach(), lpp16=l16.detach(), lpr16=r16.detach(), ep16=ep16,
                           er16=er16, pref=pref)
+    # the parameter gradients below on MIOpen's default (fast) algorithms: only the forwards above -- the window loss,
+    # eps, delta, Delta and the noise estimates built from them -- need the deterministic yardstick; the gradient bars
+    # have their slack (1.5x torch-bf16 + 1e-2)
+    det0 = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = False
     if grads16 is not None:  # the bf16 run's parameter gradients, image by image
         # fp32 leaves holding the bf16 values: autocast casts them for every conv / linear exactly as it does the
         # bf16 module weights, and the norms run in fp32 either way, so the activations match the bf16-weight run
@@ -128,6 +137,7 @@ def _oracle_window(unet_sd, mb, tr, cfg, lora_leaf=None, param_leaf=None, ref_sd
         (out * g_eps[i:i + 1]).sum().backward()
         del out
         print(f"  oracle backward image {i + 1}/{n}", flush=True)  # progress (the fp32 oracle takes minutes)
+    torch.backends.cudnn.deterministic = det0
     return ep, er, losses.mean().item(), loss16, lps
 
 
@@ -137,6 +147,7 @@ def _window(tr, buf, g):
     return tr.micro_batch(sb, 0, sb.n_micro)
 
 
+@pytest.mark.usefixtures("deterministic_yardstick")
 def test_c2_turbo_lora_window_at_1024(cuda):
     """The C2 window at 1024^2 with a LoRA large enough that the window loss leaves log 2 by far more than the bf16
     noise, and the LoRA EFFECT itself asserted: delta = eps_pol - eps_ref of every image and the per-image log-ratio
