@@ -28,19 +28,3 @@ def cuda():
     import torch
     return torch.device("cuda:0")
 
-
-@pytest.fixture
-def deterministic_yardstick():
-    """The yardsticks (the fp32 oracle and the torch-bf16 run of oracle/sdxl_ref.py) go through torch's convolutions,
-    i.e. MIOpen, whose default algorithms are not deterministic on ROCm: the same 1024^2 UNet forward differs call to
-    call by 2.3e-6 (fp32) / 1.6e-2 (bf16) max abs (tools/oracle_determinism.py), so a bar built from one torch-bf16
-    draw moves from run to run.  MIOpen's deterministic algorithms make both bit-reproducible (1.2 s per 1024^2
-    forward instead of 0.04-0.08 s, so only the single-window parity tests take them; the sweep averages draws).
-    Our kernels do not use MIOpen: the product path is unaffected."""
-    import torch
-    old = torch.backends.cudnn.deterministic
-    torch.backends.cudnn.deterministic = True
-    try:
-        yield
-    finally:
-        torch.backends.cudnn.deterministic = old
