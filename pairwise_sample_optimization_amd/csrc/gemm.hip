@@ -860,9 +860,10 @@ __global__ void gemm_splitk_reduce_kernel(GemmArgs g, int ks) {
   }
 }
 
-// Split-K plan of a dense GEMM whose output tiles leave most CUs idle while its reduction is long (the bs = 1 / GPU
+// Split-K plan of a dense GEMM whose output tiles leave CUs idle while its reduction is long (the bs = 1 / GPU
 // backward at M = 2048: 2048 x 1280 x 10240 makes 128 tiles of 128 x 160 -- half a 256-CU round at one workgroup
-// each): ks K-splits of >= 16 K-tiles each, towards 512 workgroups (two per CU), reduced in split order through a
+// each; and one-round shapes with K >= 4096): ks K-splits of >= 16 K-tiles each, towards 512 workgroups (two per
+// CU), reduced in split order through a
 // caller-owned fp32 workspace (deterministic).  The partials cost 8 M N bytes per split against 2 M N K / ks flop,
 // so only K >= 2048 qualifies.  Returns ks (0: no split) and the tile.
 struct SplitPlan { int ks, bm, bn; };
@@ -875,7 +876,11 @@ static SplitPlan gemm_split_plan(int M, int N, int K1, int K2, bool has_tail, bo
   const int nt_all = (K1 + 63) / 64 + (has_tail ? (K2 + 63) / 64 : 0);
   // variant 51: splits of >= 8 K-tiles (the short-K M = 2048 products: 2048 x 1280 x 1280 + LoRA in two)
   const int min_kt = g_gemm_variant == 51 ? 8 : 16;
-  if (tiles > 128 || nt_all < 2 * min_kt) return p;
+  // one full round of tiles (<= 256: the 4096-row products and 3x3 convs of the bs = 1 / GPU pass, K >= 4096) splits
+  // in two as well: bs = 1 step 81.56 -> 80.25 ms, C3 237.2 -> 236.5, C2 untouched (tools/bs1_variant_ab.py, one box;
+  // K >= 2560 measured the same, up to 384 tiles cost C3 1.5 %).  Variant 55 keeps the half-round rule.
+  const bool round2 = g_gemm_variant != 55 && tiles <= 256 && nt_all >= 64;
+  if ((tiles > 128 && !round2) || nt_all < 2 * min_kt) return p;
   int ks = (int)((512 + tiles - 1) / tiles);
   if (ks > nt_all / min_kt) ks = nt_all / min_kt;
   if (ks < 2) return p;
