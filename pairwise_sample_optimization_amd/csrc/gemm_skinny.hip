@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_nt_kernel(int M, int N,
   }
 }
 
-// benchmark knob (PSO_SKINNY_VARIANT): 1 = 16-row tiles x 8 K steps in flight, 2 = 32-row x 8, 3 = 16-row x 4
+// benchmark knob (PSO_SKINNY_VARIANT): 1 = 16-row tiles x 8 K steps in flight, 2 = 32-row x 8, 3 = 16-row x 4,
+// 4 = never 5 steps (the K = 1280 single-round form off)
 static int skinny_variant() {
   static int v = -1;
   if (v < 0) {
@@ -141,23 +142,48 @@ int launch_skinny(int M, int N, int K, const bf16_t* a, long lda, const bf16_t* 
                                                                 accumulate);
     return pso_check_launch("pso_gemm(skinny)");
   }
+  // K = 1280 is 40 steps of 32: with 4 steps in flight per wave that is two dependent load rounds (the second one
+  // step deep); 5 steps per wave take it in one (same per-wave step order, so the same bits).  var 4 keeps the 4.
+  // Up to 96 outputs (the fused q/k/v LoRA-down) for 16- and 32-row tiles, up to 32 for 64-row tiles (wider forms
+  // spill); forms that never take it name a form they already instantiate.
+  const bool k40 = var != 4 && (K + 31) / 32 > SK_W * 4 && (K + 31) / 32 <= SK_W * 5;
+  const bool five = NJ <= 6 && k40, five4 = NJ <= 2 && k40;
+  constexpr int U5 = NJ <= 6 ? 5 : 4, U5m = NJ <= 6 ? 5 : 0, U5d = NJ <= 2 ? 5 : 0;
   if ((long)((M + 31) / 32) * groups < 128) {
     // small M (the bs = 1 / GPU pass: 2048-row products are 64 workgroups of 32 rows): 16-row tiles, twice the
     // workgroups (bs = 1 step 23.29 vs 22.93 imgs/s same box)
     const dim3 grid((M + 15) / 16, groups);
-    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 1, 4);
-    gemm_skinny_nt_kernel<NJ, 1, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
-                                                                  accumulate);
+    if (five) {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 1, U5);
+      gemm_skinny_nt_kernel<NJ, 1, U5><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                    accumulate);
+    } else {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 1, 4);
+      gemm_skinny_nt_kernel<NJ, 1, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                    accumulate);
+    }
   } else if ((long)((M + 63) / 64) * groups >= 256) {
     const dim3 grid((M + 63) / 64, groups);
-    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 4);
-    gemm_skinny_nt_kernel<NJ, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
-                                                             accumulate);
+    if (five4) {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 4, U5d);
+      gemm_skinny_nt_kernel<NJ, 4, U5d><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                    accumulate);
+    } else {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 4);
+      gemm_skinny_nt_kernel<NJ, 4><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                               accumulate);
+    }
   } else {
     const dim3 grid((M + 31) / 32, groups);
-    pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 2);
-    gemm_skinny_nt_kernel<NJ, 2><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
-                                                             accumulate);
+    if (five) {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, %d>", NJ, 2, U5m);
+      gemm_skinny_nt_kernel<NJ, 2, U5m><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                                    accumulate);
+    } else {
+      pso_note_kernel("gemm_skinny_nt_kernel<%d, %d, 0>", NJ, 2);
+      gemm_skinny_nt_kernel<NJ, 2><<<grid, 64 * SK_W, 0, st>>>(M, N, K, a, lda, w, ldw, alpha, out, ldo, out_f32,
+                                                               accumulate);
+    }
   }
   return pso_check_launch("pso_gemm(skinny)");
 }
