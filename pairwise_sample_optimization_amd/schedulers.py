@@ -22,7 +22,7 @@ class EulerAncestralDiscreteScheduler:
         assert timestep_spacing == "trailing", "SDXL-Turbo uses trailing spacing"
         self.num_train_timesteps = num_train_timesteps
         self.alphas_cumprod = _alphas_cumprod(num_train_timesteps, beta_start, beta_end)
-        sig = np.array(((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5)
+        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
         self.sigmas = torch.from_numpy(np.concatenate([sig[::-1], [0.0]]).astype(np.float32))
         self.timesteps = None
         self.num_inference_steps = None
@@ -40,7 +40,7 @@ class EulerAncestralDiscreteScheduler:
         self.num_inference_steps = num_inference_steps
         ratio = self.num_train_timesteps / num_inference_steps
         ts = np.arange(self.num_train_timesteps, 0, -ratio).round().copy().astype(np.float32) - 1
-        sig = np.array(((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5)
+        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
         sig = np.interp(ts, np.arange(0, len(sig)), sig)
         self.sigmas = torch.from_numpy(np.concatenate([sig, [0.0]]).astype(np.float32))
         self.timesteps = torch.from_numpy(ts)
@@ -57,7 +57,7 @@ class EulerDiscreteScheduler:
     def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012):
         self.num_train_timesteps = num_train_timesteps
         self.alphas_cumprod = _alphas_cumprod(num_train_timesteps, beta_start, beta_end)
-        sig = np.array(((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5)
+        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
         self.sigmas = torch.from_numpy(np.concatenate([sig[::-1], [0.0]]).astype(np.float32))
         self.timesteps = torch.from_numpy(np.linspace(0, num_train_timesteps - 1, num_train_timesteps,
                                                       dtype=np.float32)[::-1].copy())
