@@ -547,9 +547,11 @@ def test_conv_every_variant_large(cuda, variant):
 
 @pytest.mark.parametrize("M,N,K", [(4096, 32, 1280), (4096, 96, 1280), (16384, 32, 640), (300, 100, 136),
                                    (1000, 64, 2048), (257, 128, 72), (4096, 4, 40), (32768, 32, 640),
-                                   (8192, 96, 1280), (616, 64, 2048), (20000, 48, 320)])
+                                   (8192, 96, 1280), (616, 64, 2048), (20000, 48, 320),
+                                   (2048, 96, 1280), (2048, 32, 1032), (1500, 16, 1272), (16384, 32, 1280)])
 def test_gemm_skinny_n(cuda, M, N, K):
-    """LoRA-rank products (N <= 128): bf16 out, strided A view, f32 accumulate; ragged M / K tails."""
+    """LoRA-rank products (N <= 128): bf16 out, strided A view, f32 accumulate; ragged M / K tails.  1024 < K <= 1280
+    takes the single-load-round form (5 steps per wave) on 16-, 32- and 64-row tiles, ragged K included."""
     from pairwise_sample_optimization_amd import kernels as K_
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     big = torch.randn(M, K + 24, device=cuda, generator=g).bfloat16()
