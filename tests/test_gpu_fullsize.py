@@ -266,14 +266,17 @@ def test_c2_turbo_lora_window_at_1024(cuda):
     assert rel <= bar_l
     assert rel <= 3 * propm + 1e-4
     assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
-    # the bars discriminate: the LoRA-off path (run above) fails every one of them -- by 2x at the delta / Delta level;
-    # at the loss level by 1.5x: on this window LoRA-off's loss sits 2.5e-2 from fp32 while the loss bar follows one
-    # torch-bf16 draw (prop16 5.6e-3 .. 8.2e-3 observed -> bar 1.04e-2 .. 1.43e-2), so a 2x margin passed on some boxes
-    # and failed on others (`profiles/r05_c2_window_lora_off_red.log`); the well-conditioned window below rejects
-    # LoRA-off by more than 2x at north_star's 1e-3
+    # the bars discriminate: the LoRA-off path (run above) fails every one of them -- by 2x at the delta / Delta level.
+    # At the loss level this window is bf16-noise-limited: LoRA-off's loss sits 2.5e-2 from fp32 while the loss bar
+    # follows one torch-bf16 draw (MIOpen's bf16 convolutions differ run to run: prop16 5.6e-3 .. 1.07e-2 observed ->
+    # bar 1.04e-2 .. 1.81e-2), so fixed 2x and then 1.5x margins over that bar each failed on some box
+    # (`profiles/r05_c2_window_lora_off_red.log`).  What is asserted here: the bar rejects LoRA-off, and LoRA-off's
+    # loss error is > 3x ours (ours is deterministic: 5.9e-3 vs 2.5e-2).  The well-conditioned window below rejects
+    # LoRA-off by more than 2x at north_star's 1e-3.
     assert torch.equal(lp_off[:, 0], lp_off[:, 1])                  # Delta = 0 exactly
     assert abs(loss_off.item() - math.log(2)) < 1e-6                  # loss = log 2 exactly
-    assert abs(loss_off.item() - ref_loss) / abs(ref_loss) > 1.5 * bar_l, (loss_off.item(), ref_loss, bar_l)
+    off_rel = abs(loss_off.item() - ref_loss) / abs(ref_loss)
+    assert off_rel > bar_l and off_rel > 3 * rel, (loss_off.item(), ref_loss, bar_l, rel)
     assert 1.0 > 2 * bar_d and 1.0 > 2 * bar_D                        # delta = 0 / Delta = 0 are rel 1.0 away
     assert (D32.abs() < math.log(1.1)).sum() >= n // 2                # mostly inside the clip: the gradient flows
 
