@@ -16,8 +16,10 @@ Secondary objects on the same JSON line (never the headline value):
   "lora_bs1"  the north-star operating point "bs = 1 / GPU": the C2 LoRA step at 1 pair, gas 1 (one micro-step =
               2 policy + 2 reference images in one paired pass);
   "dmd_lora"  the reference's own DMD2 recipe (config_sdxl_dmd_dpo.py: LoRA r=16, T=3, gas 4) at 1024^2;
+  "turbo_ref" the reference's own Turbo recipe (config_sdxl_turbo_dpo.py: LoRA r=32, T=3, 4 pairs, gas 2) at 512^2;
   "c5"        BASELINE configs[4] on this GPU: the DreamBooth PSO micro-step (1 instance + 1 negative, r = 16, VAE
               encode in the step), bf16 and with the fp8 forward, and their ratio;
+  "vae"       the reward-image VAE decode (8 latents -> 8 images at 1024^2) alone: ms, TF/s, GEMM-family roofline;
   "dist"      (N > 1) the backend and world size torch.distributed really runs, every rank's ms/step, and the
               bucketed all-reduce: bytes on the wire, its time alone, and the part of it left exposed after the
               backward (the rest ran under the backward).
@@ -71,7 +73,7 @@ def parse():
                          "--mode dmd --num-steps 4 --pairs 1 --gas 1)")
     ap.add_argument("--adam32", action="store_true",
                     help="fp32 AdamW instead of the reference default 8-bit AdamW (config use_8bit_adam = True)")
-    ap.add_argument("--allreduce", default="auto", choices=["auto", "fp32", "bf16"],
+    ap.add_argument("--allreduce", default="fp32", choices=["auto", "fp32", "bf16"],
                     help="gradient all-reduce wire dtype (fp32 accumulation and optimizer either way): auto = bf16 for "
                          "the full-UNet gradient (C3 / C4), fp32 for the LoRA bucket (DESIGN.md §6)")
     ap.add_argument("--allreduce-bf16", action="store_true", help="alias of --allreduce bf16")
@@ -122,7 +124,7 @@ def build(args, dev):
 def wire_dtype(args):
     if getattr(args, "allreduce_bf16", False):
         return torch.bfloat16
-    return {"auto": "auto", "fp32": torch.float32, "bf16": torch.bfloat16}[getattr(args, "allreduce", "auto")]
+    return {"auto": "auto", "fp32": torch.float32, "bf16": torch.bfloat16}[getattr(args, "allreduce", "fp32")]
 
 
 def one_step(tr, buf, g, graph=False):
@@ -150,11 +152,16 @@ def roofline(tr, buf, g):
     time per step): achieved = its algorithmic 2*M*N*K flop per launch / its average launch duration.  The whole
     family is reported beside it.  traffic = HBM bytes per launch of that kernel from the two PMC passes
     (tools/gpu_full.sh -> tools/parse_prof.py), used only when they were collected on these exact sources."""
+    return family_roofline(lambda: one_step(tr, buf, g))
+
+
+def family_roofline(fn):
+    """roofline() of any callable: fn runs once with every GEMM-family launch timed by its own HIP event pair."""
     from collections import defaultdict
     from pairwise_sample_optimization_amd import kernels as K
     K.PROFILE = []
     side, K.SideStream.enabled_any = K.SideStream.enabled_any, False  # serial launches: each event pair times one kernel
-    one_step(tr, buf, g)
+    fn()
     torch.cuda.synchronize()
     rec, K.PROFILE = K.PROFILE, None
     K.SideStream.enabled_any = side
@@ -388,6 +395,43 @@ def c5_metric(dev, steps=8, warmup=2):
     return out
 
 
+def vae_metric(dev, n_img=8, steps=5, warmup=1):
+    """SURVEY §8a a7 on this GPU: the reward-image VAE decode of one epoch's sampled latents (2 P gas = 8 images at
+    1024^2, DP/sdxl_turbo_with_logprob.py:154-155: decode of latents / scaling_factor; random-init weights), timed alone
+    with HIP events over `steps` decodes; its GEMM-family roofline from one profiled decode.  10.49 TFLOP per image
+     -> mfma_frac."""
+    from pairwise_sample_optimization_amd.vae import AutoencoderKL, VAEConfig
+    with torch.device(dev):
+        vae = AutoencoderKL(VAEConfig())
+    vae.init_weights(0)
+    vae.prepare()
+    g = torch.Generator(device=dev).manual_seed(7)
+    lat = torch.randn(n_img, 128, 128, 4, device=dev, generator=g)   # the trajectory buffer's NHWC fp32 latents
+    for _ in range(warmup):
+        vae.decode_latents_nhwc(lat)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        vae.decode_latents_nhwc(lat)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    tf = VAE_DEC_TFLOP_PER_IMG * n_img
+    rf = family_roofline(lambda: vae.decode_latents_nhwc(lat))
+    out = {"images": n_img, "ms_per_decode": round(ms, 2), "ms_per_image": round(ms / n_img, 3),
+           "tflop_per_decode": round(tf, 2), "achieved_tflops": round(tf / (ms * 1e-3), 1),
+           "mfma_frac": round(tf / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4),
+           "roofline": {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "avg_launch_us",
+                                           "launches_per_step", "share_of_family_time", "family")},
+           "workload": "VAE decode (SDXL AutoencoderKL decoder, random-init) of 8 latents 128x128 -> 8 images 1024^2, "
+                       "bf16, one launch sequence per call"}
+    del vae, lat
+    torch.cuda.empty_cache()
+    log(f"[bench] vae: {out['ms_per_decode']} ms per {n_img}-image decode ({out['achieved_tflops']} TF/s)")
+    return out
+
+
 def dist_report(tr, dev, dt_rank, steps):
     """What torch.distributed really ran (backend, world) and the overlap of the gradient all-reduce with the
     backward: exposed = the compute stream's wait for RCCL after the window's last backward (GradBuckets.finish,
@@ -537,8 +581,18 @@ def main():
                                workload="the reference's own DMD2 recipe (config_sdxl_dmd_dpo.py): LoRA r=16, 4-step "
                                         "sampler (T=3), 1 pair / micro-step, gas 4 (12 micro-steps = 24 images per "
                                         "optimizer step, passes of <= 16 images), 8-bit AdamW, bf16, 1024^2")
+        log("[bench] turbo_ref ...")
+        res["turbo_ref"] = dict(sub_config(args, dev, "turbo_ref", max(1, args.extra_steps - 1), warmup=1,
+                                           mode="turbo", num_steps=4, pairs=4, gas=2, rank=32, res=512,
+                                           full_unet=False),
+                                workload="the reference's own Turbo recipe (online_pso_sdxl_turbo.sh, "
+                                         "config_sdxl_turbo_dpo.py): LoRA r=32, 4-step sampler (T=3), 4 pairs / "
+                                         "micro-step, gas 2 (6 micro-steps = 48 images per optimizer step, passes of "
+                                         "<= 16 images), 8-bit AdamW, bf16, 512^2 (T:324-332)")
         log("[bench] c5 ...")
         res["c5"] = c5_metric(dev)
+        log("[bench] vae ...")
+        res["vae"] = vae_metric(dev)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -236,6 +236,9 @@ def dequant_rows_fp8(q, e):
     return q.view(torch.float8_e4m3fn).float() * torch.exp2(e.float() - 127.0)[:, None]
 
 
+FP8_LAUNCHES = [0]  # pso_gemm_fp8 calls issued by this process (tests assert that an fp8 path really ran)
+
+
 def gemm_fp8(a, w, *, a2=None, w2=None, tail_rows=0, tail_group_n=0, alpha=1.0, bias=None, resid=None, out=None,
              geglu=False, out_pre=None, pre_rows=0):
     """fp8 forward GEMM (pso_gemm_fp8): a = (q [M, K], e [M]) and w = (q [N, K], e [N]) from quant_rows_fp8, likewise
@@ -243,6 +246,7 @@ def gemm_fp8(a, w, *, a2=None, w2=None, tail_rows=0, tail_group_n=0, alpha=1.0, 
     geglu: the GEGLU epilogue of gemm_geglu on interleaved weight rows (out [M, N/2], out_pre rows < pre_rows)."""
     (aq, ae), (wq, we) = a, w
     require_cuda(aq, wq)
+    FP8_LAUNCHES[0] += 1
     M, Kd = aq.shape
     N = wq.shape[0]
     assert wq.shape[1] == Kd and aq.dtype == torch.uint8 and wq.dtype == torch.uint8

@@ -290,7 +290,7 @@ class PSOTrainer:
     def __init__(self, unet, mode="turbo", num_steps=2, beta=50.0, clip_eps=0.1, lr=1e-5, betas=(0.9, 0.999),
                  weight_decay=1e-6, adam_eps=1e-8, max_grad_norm=1.0, gradient_accumulation_steps=1,
                  train_batch_size=1, num_reward=1, process_group=None, max_pass_images=16, ref_unet=None,
-                 latent_dtype=torch.float32, allreduce_dtype="auto", use_8bit_adam=False, overlap_sync=None,
+                 latent_dtype=torch.float32, allreduce_dtype=None, use_8bit_adam=False, overlap_sync=None,
                  bucket_mb=32.0):
         self.unet = unet
         if mode not in ("turbo", "dmd"):
@@ -332,10 +332,11 @@ class PSOTrainer:
         self.overlap_sync = (self.world > 1) if overlap_sync is None else bool(overlap_sync)
         if self.overlap_sync and not (dist.is_available() and dist.is_initialized()):
             raise ValueError("overlap_sync needs an initialised process group")
-        # allreduce_dtype=torch.bfloat16: bf16 on the wire, fp32 accumulation and optimizer (GradBuckets).  "auto" (the
-        # default) puts the full-UNet gradient (C3 / C4: 10.3 GB fp32 per sync, 18 GB of ring traffic per rank at 8
-        # ranks) on a bf16 wire and keeps the LoRA bucket (185.8 MB at r = 32) fp32 as DDP does; torch.float32 / None
-        # force the fp32 wire
+        # The default (None / torch.float32) is the reference's wire: DDP's fp32 all-reduce (T:228-233).  Opt-in:
+        # torch.bfloat16 puts the gradient on a bf16 wire (fp32 accumulation and optimizer, GradBuckets); "auto" does
+        # that for the full-UNet gradient only (C3 / C4: 10.3 GB fp32 per sync, 18 GB of ring traffic per rank at 8
+        # ranks) and keeps the LoRA bucket fp32.  RCCL's ring re-rounds every partial sum on a bf16 wire, so its error
+        # grows with the world size
         if isinstance(allreduce_dtype, str):
             if allreduce_dtype != "auto":
                 raise ValueError(f"allreduce_dtype must be a torch dtype, None or 'auto', got {allreduce_dtype!r}")

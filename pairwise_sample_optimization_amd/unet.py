@@ -316,6 +316,59 @@ def _tn_stacked(fg, lins, dy, x):
 # ======================================================================================================================
 # LoRA state: flat fp32 masters + flat fp32 grads (the all-reduce bucket), bf16 working copies
 # ======================================================================================================================
+LORA_TARGETS = ("to_k", "to_q", "to_v", "to_out.0")  # T:342, D:365, DB:1324
+
+
+class LoraConfig:
+    """The fields of peft 0.11's `LoraConfig` that shape a UNet adapter, with peft's defaults (peft is not a
+    dependency here; `add_adapter` also takes peft's own object or any namespace with these attribute names)."""
+
+    def __init__(self, r=8, lora_alpha=8, target_modules=None, init_lora_weights=True, lora_dropout=0.0,
+                 bias="none", use_rslora=False, use_dora=False, fan_in_fan_out=False, modules_to_save=None,
+                 layers_to_transform=None, layers_pattern=None, rank_pattern=None, alpha_pattern=None, **kw):
+        self.r, self.lora_alpha, self.target_modules = r, lora_alpha, target_modules
+        self.init_lora_weights, self.lora_dropout, self.bias = init_lora_weights, lora_dropout, bias
+        self.use_rslora, self.use_dora, self.fan_in_fan_out = use_rslora, use_dora, fan_in_fan_out
+        self.modules_to_save, self.layers_to_transform, self.layers_pattern = modules_to_save, layers_to_transform, \
+            layers_pattern
+        self.rank_pattern, self.alpha_pattern = rank_pattern or {}, alpha_pattern or {}
+        for k, v in kw.items():  # task_type, inference_mode, revision, ...: no effect on the adapter arithmetic
+            setattr(self, k, v)
+
+
+def check_lora_config(cfg):
+    """(r, lora_alpha) of a peft-style LoraConfig, after checking that it asks for the adapters the reference trains:
+    LoRA (not DoRA / rsLoRA) on exactly to_q / to_k / to_v / to_out.0 of every attention, gaussian init, no dropout, no
+    bias, no per-module rank / alpha patterns, no extra trained modules.  A field the object does not carry counts as
+    the reference's value (namespace configs: SimpleNamespace(r=..., lora_alpha=...)); a field that differs raises
+    ValueError naming it -- the kernels would otherwise train other adapters than the config asks for."""
+    def get(name, ref):
+        return getattr(cfg, name, ref)
+
+    r = get("r", 32)
+    if isinstance(r, bool) or not isinstance(r, int) or r <= 0 or r % 8:
+        raise ValueError(f"LoraConfig.r must be a positive multiple of 8 (the rank kernels' granule), got {r!r}")
+    alpha = get("lora_alpha", r)
+    if isinstance(alpha, bool) or not isinstance(alpha, (int, float)) or not alpha > 0:
+        raise ValueError(f"LoraConfig.lora_alpha must be a positive number, got {alpha!r}")
+    tm = get("target_modules", LORA_TARGETS)
+    if isinstance(tm, str) or tm is None or sorted(tm) != sorted(LORA_TARGETS) or len(set(tm)) != len(tm):
+        raise ValueError(f"LoraConfig.target_modules must be {list(LORA_TARGETS)} (T:342), got {tm!r}")
+    init = get("init_lora_weights", "gaussian")
+    if init != "gaussian" or isinstance(init, bool):
+        raise ValueError(f"LoraConfig.init_lora_weights must be 'gaussian' (T:341), got {init!r}")
+    checks = (("lora_dropout", 0.0, lambda v: v == 0), ("bias", "none", lambda v: v == "none"),
+              ("use_rslora", False, lambda v: v is False), ("use_dora", False, lambda v: v is False),
+              ("fan_in_fan_out", False, lambda v: v is False), ("modules_to_save", None, lambda v: not v),
+              ("layers_to_transform", None, lambda v: v is None), ("layers_pattern", None, lambda v: v is None),
+              ("rank_pattern", {}, lambda v: not v), ("alpha_pattern", {}, lambda v: not v),
+              ("megatron_config", None, lambda v: v is None), ("loftq_config", {}, lambda v: not v))
+    for name, ref, ok in checks:
+        v = get(name, ref)
+        if not ok(v):
+            raise ValueError(f"LoraConfig.{name}={v!r} is not implemented (the reference uses {ref!r})")
+    return r, alpha
+
 class LoraState:
     """peft LoraConfig(r, lora_alpha=r, init_lora_weights="gaussian", target_modules=[to_k,to_q,to_v,to_out.0])
     (T:338-345): A ~ N(0, 1/r) [r, in], B = 0 [out, r], scaling alpha/r.
@@ -1086,9 +1139,10 @@ class UNet2DConditionModel(nn.Module):
                 yield name, m
 
     def add_adapter(self, lora_config):
-        """peft LoraConfig(r, lora_alpha, init_lora_weights='gaussian', target_modules=[to_k,to_q,to_v,to_out.0])."""
-        r = getattr(lora_config, "r", 32)
-        alpha = getattr(lora_config, "lora_alpha", r)
+        """peft LoraConfig(r, lora_alpha, init_lora_weights='gaussian', target_modules=[to_k,to_q,to_v,to_out.0])
+        (T:338-345, D:361-366, DB:1319-1325).  The kernels implement exactly that adapter set: every LoraConfig field
+        is checked (check_lora_config) and anything else raises instead of training other adapters than asked."""
+        r, alpha = check_lora_config(lora_config)
         blocks = [(name, blk.dim, blk.attn2.kv_dim) for name, blk in self._attn_modules()]
         dev = self.conv_in.weight.device
         self.lora = LoraState(blocks, r, alpha, dev)
@@ -1244,23 +1298,21 @@ class UNet2DConditionModel(nn.Module):
         quantised once and cached.  The LoRA sB stacks (version > 0) change at every optimizer step: eager forwards
         re-quantise them once per LoRA version into buffers allocated once; under a hipGraph capture every forward
         re-quantises, so the capture records the quantisation kernel and each replay reads the current LoRA weights (a
-        version-keyed cache hit would record nothing and replay the capture-time copies)."""
+        version-keyed cache hit would record nothing and replay the capture-time copies).  A quantisation recorded by
+        a capture has not run yet, so its entry is marked stale (-1): the next eager forward re-quantises."""
+        capturing = torch.cuda.is_current_stream_capturing()
         hit = self._fp8_cache.get(key)
-        if version == 0:
-            if hit is None:
-                hit = (0, K.quant_rows_fp8(w))
-                self._fp8_cache[key] = hit
-            return hit[1]
-        if hit is None or hit[1][0].shape != w.shape:
-            hit = (version, K.quant_rows_fp8(w))
-            self._fp8_cache[key] = hit
-            return hit[1]
-        q, e = hit[1]
-        if hit[0] == version and not torch.cuda.is_current_stream_capturing():
-            return hit[1]  # eager: this LoRA version is already quantised (a capture re-records the kernel)
-        K.quant_rows_fp8(w, q=q, e=e)
-        self._fp8_cache[key] = (version, hit[1])
-        return hit[1]
+        if hit is not None and hit[1][0].shape == w.shape:
+            # a valid entry serves eager forwards, and captures of the frozen weights (computed eagerly before)
+            if hit[0] == version and (version == 0 or not capturing):
+                return hit[1]
+            q, e = hit[1]
+            K.quant_rows_fp8(w, q=q, e=e)
+            buf = hit[1]
+        else:
+            buf = K.quant_rows_fp8(w)
+        self._fp8_cache[key] = (-1 if capturing else version, buf)
+        return buf
 
     def kv_text(self, rt, C):
         """K/V of the text tokens for every block of width C: ([rows, n*2C], LoRA down-projection [policy rows, n*2r]

@@ -120,9 +120,9 @@ def main_full(args):
     unet.prepare()
     P = 1
     tr = PSOTrainer(unet, mode="dmd", num_steps=4, gradient_accumulation_steps=1, train_batch_size=P,
-                    ref_unet=ref_unet, use_8bit_adam=True, lr=1e-4)
+                    ref_unet=ref_unet, use_8bit_adam=True, lr=1e-4, allreduce_dtype="auto")
     assert tr.world == world and tr.buckets is not None
-    assert tr.allreduce_dtype == torch.bfloat16  # full-UNet default: bf16 wire
+    assert tr.allreduce_dtype == torch.bfloat16  # "auto" (opt-in): the full-UNet gradient on a bf16 wire
     tr.buckets = GradBuckets(unet, fg.grad, bucket_mb=0.5, wire_dtype=tr.allreduce_dtype)  # several buckets
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)
     enc = torch.randn(P, 77, cfg.cross_attention_dim, device=dev, generator=g).bfloat16()

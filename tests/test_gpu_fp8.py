@@ -104,7 +104,7 @@ def test_gemm_fp8_geglu(cuda, M, Fd, K, pre_rows):
 
 
 @pytest.mark.parametrize("which", ["sdxl32", "sdxl64"])
-def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which):
+def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which, monkeypatch):
     """The whole SDXL UNet with enable_fp8_forward() (fp8 cross q and GEGLU proj; bf16 elsewhere; bf16 backward)
     against the fp32 oracle: eps and every LoRA gradient.  Bars: the bf16 path's (3e-2 / 5e-2) widened by the e4m3
     operand rounding (3 mantissa bits: ~2^-5 relative per operand, averaged over K).  The gradients move more than eps
@@ -112,7 +112,12 @@ def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which):
     0.117 / 0.14): the backward runs on the fp8 forward's cross q and GEGLU pre-activations, so their rounding enters
     the attention / GEGLU backward products."""
     from test_gpu_unet import _oracle, _setup
+    from pairwise_sample_optimization_amd import kernels as K
+    from pairwise_sample_optimization_amd import unet as U
     from pairwise_sample_optimization_amd.unet import UNetConfig
+    # the occupancy rule (FP8_MIN_TILES = 192 tiles of 256 x 256) keeps every product of these small UNets on bf16:
+    # lift it so the e4m3 kernels run here (ADVICE r5)
+    monkeypatch.setattr(U, "FP8_MIN_TILES", 0)
     cfg = UNetConfig.sdxl(32 if which == "sdxl32" else 64)
     unet, sample, t, enc, text, tid = _setup(cuda, cfg, r=16)  # rank 16 (the DreamBooth recipe): fp8 LoRA tails
     add = {"text_embeds": text, "time_ids": tid}
@@ -120,7 +125,10 @@ def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which):
         ref = _oracle(unet, cfg, sample, t, enc, text, tid, True)
         bf = unet(sample, t, enc, added_cond_kwargs=add).sample
         unet.enable_fp8_forward()
+        n0 = K.FP8_LAUNCHES[0]
         f8 = unet(sample, t, enc, added_cond_kwargs=add).sample
+        assert K.FP8_LAUNCHES[0] > n0, "the fp8 forward must run e4m3 GEMMs"
+    assert not torch.equal(f8, bf), "fp8 and bf16 forwards gave the same bits: no e4m3 product ran"
     e_bf, e_f8 = _rel(bf, ref), _rel(f8, ref)
     G = torch.randn(sample.shape, device=cuda, generator=torch.Generator(device="cuda").manual_seed(5))
     unet.lora.grad.zero_()

@@ -635,6 +635,150 @@ def test_dmd_reference_lora_config_window_at_1024(cuda):
     assert abs(tot["off"] - tot["ref"]) / tot["ref"] > 2e-3              # LoRA-off rejected by > 2x the bar
 
 
+def test_turbo_reference_lora_config_window_at_512(cuda):
+    """The reference's own Turbo recipe at its own resolution (online_pso_sdxl_turbo.sh:3-15, config_sdxl_turbo_dpo.py
+    via PSOTrainer.from_config: LoRA r = 32 on to_q / to_k / to_v / to_out.0 (peft-style LoraConfig, T:338-343),
+    4-step sampler -> T = 3, 4 pairs per micro-step, gradient_accumulation_steps 2 -> a window of 6 micro-steps = 24
+    pairs, 8-bit AdamW, beta 50, eps 0.1; 512^2 = 64 x 64 latents, T:324-332) run as the trainer runs it (passes of at
+    most 16 policy images: 3 passes of 2 micro-steps) against the fp32 oracle.
+
+    Turbo transitions at N = 4 amplify eps errors less than C2's N = 2 (dmu/deps / sigma_up = dt / sigma_up = -3.4 /
+    -2.3 / -2.1 at t = 999 / 749 / 499, against -9.0), but their log-ratios are as small, so the window is built the way
+    the C2 well-conditioned window is: every pair's loser (member 0) takes a transition pushed along the
+    policy's LoRA effect until its log-ratio saturates the reference's clamp (T:846, exact in any precision) and the
+    winner's (member 1) log-ratio sits at -0.02, well inside the clip; both from the fp32 oracle's eps, the push chosen
+    per image from the fp32 LoRA effect: Delta(k) = (2k - 1) m for a transition at x + dt (eps_ref + k delta) + noise,
+    m = mean((dt delta)^2) / (2 sigma_up^2).  The loss is then carried by the winners' log-ratios alone.
+    Bars: loss within north_star's 1e-3 rel; eps, delta, Delta and the 1,120 LoRA gradients within 1.5x the torch-bf16
+    distance + floor; the LoRA-off path (loss = log 2) rejected by > 2x the loss bar."""
+    from oracle import sdxl_ref
+    from pairwise_sample_optimization_amd import kernels as K
+    from pairwise_sample_optimization_amd.config import config_sdxl_turbo_dpo
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import LORA_TARGETS, LoraConfig, UNet2DConditionModel, UNetConfig
+    c = config_sdxl_turbo_dpo.get_config()
+    h = 64
+    cfg = UNetConfig.sdxl(h)
+    with torch.device(cuda):
+        unet = UNet2DConditionModel(cfg)
+    unet.init_weights(0)
+    unet.add_adapter(LoraConfig(r=c.train.lora_rank, lora_alpha=c.train.lora_rank, init_lora_weights="gaussian",
+                                target_modules=list(LORA_TARGETS)))
+    # B std 3e-2: at dt / sigma_up ~ 2-3.4 the LoRA effect's m is ~1e-2 (C2's 1.5e-2 gives 4.5e-2 at ratio 9)
+    unet.lora.init_gaussian(seed=0, b_std=3e-2)
+    unet.prepare()
+    tr = PSOTrainer.from_config(unet, c, mode="turbo")
+    assert (tr.T, tr.P, tr.gas, tr.gas_total, unet.lora.r) == (3, 4, 2, 6, 32) and tr.adam8 is not None
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(4000)
+    Bp = tr.P * tr.gas
+    enc = torch.randn(Bp, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(Bp, 1280, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(512, 0, cuda).repeat(Bp, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, h, generator=g,
+                          reward_fn=lambda img: torch.rand(img.shape[0], device=cuda, generator=g))
+    sb = tr.shuffle(buf, generator=g)
+    assert sb.n_micro == 6
+    rw = torch.zeros_like(sb.rewards)
+    rw.view(rw.shape[0], 2, -1)[:, 1] = 1.0  # the winner is member 1 of every pair (sample_compare, T:401-416)
+    sb.rewards = rw
+    per_pass = max(1, tr.max_pass_images // (2 * tr.P))
+    passes = [(s0, min(per_pass, sb.n_micro - s0)) for s0 in range(0, sb.n_micro, per_pass)]
+    assert passes == [(0, 2), (2, 2), (4, 2)]
+    st = unet.lora
+    st.grad.zero_()
+    sd = sdxl_ref.sd_to(unet.state_dict(), cuda)
+    leaf = {k: v.float().clone().requires_grad_(True) for k, v in st.state_dict_peft().items()}
+    g16 = {}
+    tot = dict(mine=0.0, ref=0.0, r16=0.0, off=0.0)
+    Dm_all, D32_all, D16_all, ms_all, resolved, t_all = [], [], [], [], [], []
+    rds, rd16s, eps_rel = [], [], []
+    q = lambda t: t.bfloat16().float()
+    lo, hi = math.log(1 - tr.clip_eps), math.log(1 + tr.clip_eps)
+    for s0, cnt in passes:
+        mb = tr.micro_batch(sb, s0, cnt)
+        n = mb.unet_in.shape[0]
+        assert n == 16
+        ep0, er0 = _oracle_eps32(cfg, unet, mb, cuda)
+        cf = mb.coef
+        su, dt = cf[:, 1].view(-1, 1, 1, 1), cf[:, 2].view(-1, 1, 1, 1)
+        xs = mb.x.permute(0, 3, 1, 2)
+        dlt = q(ep0) - q(er0)
+        m = ((dt * dlt) ** 2).mean((1, 2, 3)) / (2 * su.view(-1) ** 2)
+        ms_all.append(m)
+        member = torch.arange(n, device=cuda) % 2
+        tgt = torch.where(member == 0, torch.full_like(m, hi + 0.08), torch.full_like(m, -0.02))
+        k = (tgt / m + 1) / 2
+        # a pair whose LoRA effect bf16 cannot resolve (m < 2e-3: |delta| near the bf16 resolution of eps -- the first
+        # run of this test had m down to 4e-6 at some timesteps, and a push by k ~ 1e4 there made the loser's Delta 30 %
+        # wrong in ANY bf16 forward: mine and torch-bf16 both 1.9e-2 off in loss) keeps both members at the reference
+        # mean + noise: Delta ~ 0, loss ~ log 2, exact to bf16's resolution of that pair
+        m_pair = m.view(-1, 2).min(1).values.repeat_interleave(2)
+        k = torch.where(m_pair >= 2e-3, k, torch.zeros_like(k)).view(-1, 1, 1, 1)
+        resolved.append(m_pair >= 2e-3)
+        t_all.append(mb.t.float())
+        xi = torch.randn(xs.shape, device=cuda, generator=torch.Generator(device="cuda").manual_seed(191 + s0))
+        xp = xs + dt * (q(er0) + k * dlt) + 0.25 * su * xi
+        mb.x_next = xp.permute(0, 2, 3, 1).contiguous()
+        del ep0, er0, dlt
+        with torch.no_grad():
+            eps_both, _ = unet.forward_nhwc(mb.unet_in, mb.t, mb.enc, mb.pooled, mb.tid, save=False, paired_ref=True)
+        pref_k = K.preference(mb.rewards, 0)
+        assert torch.equal(pref_k[:, 1], torch.ones_like(pref_k[:, 1]))
+        ws = K.pair_loss_ws(n // 2, mb.x[0].numel(), cuda)
+        loss_k, lp_mine = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[:n].contiguous(),
+                                          eps_both[n:].contiguous(), mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
+        loss_off, _ = K.pair_loss_fwd(tr.mode, mb.x, mb.x_next, eps_both[n:].contiguous(), eps_both[n:].contiguous(),
+                                      mb.coef, pref_k, tr.beta, tr.clip_eps, ws)
+        mine_loss = tr.micro_step(mb).item()
+        assert abs(mine_loss - loss_k.item()) <= 1e-6 * abs(loss_k.item())  # training pass == inference pass
+        g16p = {}
+        ep, er, ref_loss, loss16, lps = _oracle_window(sd, mb, tr, cfg, lora_leaf=leaf, grads16=g16p)
+        for k_, v_ in g16p.items():  # the torch-bf16 window gradient: summed over the passes
+            g16[k_] = v_ if k_ not in g16 else g16[k_] + v_
+        e_pol, e_ref = K.nhwc_to_nchw(eps_both[:n]), K.nhwc_to_nchw(eps_both[n:])
+        eps_rel += [_rel(e_pol, ep), _rel(e_ref, er)]
+        d32 = q(ep) - q(er)
+        rds.append(_rel(e_pol - e_ref, d32))
+        rd16s.append(_rel(q(lps.ep16) - q(lps.er16), d32))
+        Dm_all.append((lp_mine[:, 0] - lp_mine[:, 1]).reshape(-1))
+        D32_all.append((lps.lpp - lps.lpr).reshape(-1))
+        D16_all.append((lps.lpp16 - lps.lpr16).reshape(-1))
+        for k_, v_ in (("mine", mine_loss), ("ref", ref_loss), ("r16", loss16), ("off", loss_off.item())):
+            tot[k_] += v_ * cnt / sb.n_micro  # window loss = mean over its micro-steps
+        _say(f"  turbo recipe pass {s0 // per_pass + 1}/{len(passes)} done")
+    Dm, D32, D16, mm = torch.cat(Dm_all), torch.cat(D32_all), torch.cat(D16_all), torch.cat(ms_all)
+    res, tt = torch.cat(resolved).view(-1, 2)[:, 0], torch.cat(t_all)
+    m_by_t = {int(t): (mm[tt == t].min().item(), mm[tt == t].max().item()) for t in torch.unique(tt).tolist()}
+    rD, rD16 = _rel(Dm, D32), _rel(D16, D32)
+    rel = abs(tot["mine"] - tot["ref"]) / abs(tot["ref"])
+    rel16 = abs(tot["r16"] - tot["ref"]) / abs(tot["ref"])
+    mine = st.grad_dict_peft()
+    den = sum((v.grad ** 2).sum().item() for v in leaf.values())
+    grel = (sum(((mine[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    grel16 = (sum(((g16[k] - v.grad) ** 2).sum().item() for k, v in leaf.items()) / den) ** 0.5
+    rd, rd16 = max(rds), max(rd16s)
+    print(f"Turbo reference config @512 (r=32, P=4, gas 2, T=3, 48 images in 3 passes): LoRA effect m by timestep "
+          f"{m_by_t}; {int(res.sum())} of {res.numel()} pairs resolved (pushed); eps rel max {max(eps_rel):.2e}; delta rel mine {rd:.3e} "
+          f"torch-bf16 {rd16:.3e}; Delta fp32 {D32.tolist()} mine {Dm.tolist()} rel mine {rD:.3e} torch-bf16 "
+          f"{rD16:.3e}; window loss mine {tot['mine']:.6f} fp32 {tot['ref']:.6f} torch-bf16 {tot['r16']:.6f} LoRA-off "
+          f"{tot['off']:.6f} rel(mine) {rel:.2e} rel(torch-bf16) {rel16:.2e}; LoRA grad rel mine {grel:.3e} "
+          f"torch-bf16 {grel16:.3e} over {len(leaf)} tensors")
+    # the window is what it is built to be: losers saturate the clamp, winners inside it, pair gaps >> Delta noise
+    D2, Dm2 = D32.view(-1, 2), Dm.view(-1, 2)
+    assert res.sum() >= res.numel() // 2 and (mm < 0.2).all()
+    assert (D2[res, 0] > hi + 0.02).all() and (D2[res, 1] > lo + 0.03).all() and (D2[res, 1] < hi - 0.03).all()
+    assert (Dm2[res, 0] > hi).all()                                      # our losers saturate the clamp too
+    assert ((D2[res, 0] - D2[res, 1]).abs() > 100 * (Dm2[res, 1] - D2[res, 1]).abs().max()).all()
+    assert (D2[~res].abs() < 1e-2).all()                                # unresolved pairs: Delta ~ 0 (loss ~ log 2)
+    assert max(eps_rel) < 3e-2
+    assert rd <= 1.5 * rd16 + 2e-2 and rD <= 1.5 * rD16 + 2e-2
+    assert rel <= 1e-3                                                   # north_star
+    assert grel <= 1.5 * grel16 + 1e-2 and grel < 1e-1
+    assert abs(tot["off"] - math.log(2)) < 1e-6
+    assert abs(tot["off"] - tot["ref"]) / tot["ref"] > 2e-3              # LoRA-off rejected by > 2x the bar
+
+
 @pytest.mark.parametrize("P", [1, 2])
 def test_c3_dmd_full_unet_window_at_1024(cuda, P):
     """C3 (P = 1, one GPU) and C4's per-rank workload (P = 2 pairs per GPU of the 8-GPU global 16, D:777-864): the

@@ -85,3 +85,32 @@ def test_trainer_from_config_latent_dtype_follows_mixed_precision():
         warnings.simplefilter("always")
         Probe.from_config(None, c, mode="dmd", latent_dtype=torch.float32)
     assert seen["latent_dtype"] == torch.float32 and any("mixed_precision" in str(x.message) for x in w)
+
+
+def test_add_adapter_honours_or_rejects_lora_config():
+    """The reference's LoraConfig (T:338-343: r, lora_alpha = r, init 'gaussian', to_k / to_q / to_v / to_out.0) is
+    accepted in peft's own form; any field that would make peft train other adapters raises instead of being ignored."""
+    from pairwise_sample_optimization_amd.unet import LoraConfig, UNet2DConditionModel, UNetConfig
+    with torch.device("meta"):
+        u = UNet2DConditionModel(UNetConfig.sdxl())
+    ref = dict(r=16, lora_alpha=16, init_lora_weights="gaussian", target_modules=["to_k", "to_q", "to_v", "to_out.0"])
+    st = u.add_adapter(LoraConfig(**ref))
+    assert (st.r, st.scale) == (16, 1.0)
+    st = u.add_adapter(LoraConfig(**dict(ref, lora_alpha=32, target_modules=("to_out.0", "to_v", "to_q", "to_k"),
+                                         task_type=None, inference_mode=False)))
+    assert (st.r, st.scale) == (16, 2.0)
+    bad = [dict(target_modules=["to_q", "to_v"]), dict(target_modules=["to_k", "to_q", "to_v", "to_out.0", "proj_in"]),
+           dict(target_modules="to_q|to_k|to_v|to_out.0"), dict(target_modules=None), dict(init_lora_weights=True),
+           dict(init_lora_weights="pissa"), dict(use_dora=True), dict(use_rslora=True), dict(lora_dropout=0.1),
+           dict(bias="all"), dict(rank_pattern={"to_q": 4}), dict(alpha_pattern={"to_q": 4}),
+           dict(modules_to_save=["conv_in"]), dict(layers_to_transform=[0]), dict(r=12), dict(r=0), dict(lora_alpha=0)]
+    for b in bad:
+        with pytest.raises(ValueError):
+            u.add_adapter(LoraConfig(**dict(ref, **b)))
+    # namespace configs: absent fields are the reference's, present ones are checked the same way
+    assert u.add_adapter(SimpleNamespace(r=8, lora_alpha=8)).r == 8
+    with pytest.raises(ValueError):
+        u.add_adapter(SimpleNamespace(r=8, lora_alpha=8, target_modules=["to_q"]))
+    # peft's default (init True, no target_modules) is not the reference's adapter either
+    with pytest.raises(ValueError):
+        u.add_adapter(LoraConfig(r=8, lora_alpha=8))
