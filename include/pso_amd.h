@@ -360,6 +360,14 @@ int pso_im2col3(int B, int H, int W, int C, const void* in, void* out, int Kp, v
 int pso_colsum_acc(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* stream);
 int pso_layer_norm_dparam(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
                           float* dgamma, float* dbeta, void* stream);
+/* Ordered forms of the two sums above (no float atomics: per-row-block partials in a caller-owned workspace, added in
+ * row-block order -- bit-reproducible full-UNet gradients).  The workspace sizes are *_ws_bytes. */
+size_t pso_colsum_acc_ws_bytes(long M, int N, long rows_per_group);
+int pso_colsum_acc_ws(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* ws,
+                      size_t ws_bytes, void* stream);
+size_t pso_layer_norm_dparam_ws_bytes(int M, int C);
+int pso_layer_norm_dparam_ws(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                             float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 int pso_im2col_conv(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,
                     int stride, int pad, void* out, long ldo, void* stream);
 int pso_sumpool2(int B, int H, int W, int C, const void* in, const void* dadd, void* out, void* stream);

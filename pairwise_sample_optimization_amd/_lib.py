@@ -105,6 +105,10 @@ SIGNATURES = {
     "pso_im2col3": (ci, [ci, ci, ci, ci, vp, vp, ci, vp]),
     "pso_colsum_acc": (ci, [cl, ci, vp, cl, cl, vp, cl, vp]),
     "pso_layer_norm_dparam": (ci, [ci, ci, vp, cl, vp, cl, vp, vp, vp, vp]),
+    "pso_colsum_acc_ws_bytes": (csz, [cl, ci, cl]),
+    "pso_colsum_acc_ws": (ci, [cl, ci, vp, cl, cl, vp, cl, vp, csz, vp]),
+    "pso_layer_norm_dparam_ws_bytes": (csz, [ci, ci]),
+    "pso_layer_norm_dparam_ws": (ci, [ci, ci, vp, cl, vp, cl, vp, vp, vp, vp, csz, vp]),
     "pso_im2col_conv": (ci, [ci, ci, vp, ci, vp, ci, ci, ci, ci, ci, ci, ci, vp, cl, vp]),
     "pso_sumpool2": (ci, [ci, ci, ci, ci, vp, vp, vp, vp]),
     "pso_axpby": (ci, [cl, cf, vp, cf, vp, vp, vp]),

@@ -5,6 +5,8 @@
 //   pso_colsum_acc         out[g][n] += sum of x[m][n] over the rows m of group g (bias gradients: one group; the
 //                          per-image time-embedding row-bias gradients of the resnets: one group per image)
 //   pso_layer_norm_dparam  dgamma[c] += sum_m dy[m][c] * (x[m][c] - mean_m) * rstd_m,  dbeta[c] += sum_m dy[m][c]
+//   (the *_ws forms: the same sums reduced in a fixed order through a caller-owned workspace -- no float atomics;
+//   the product path uses them, so the full-UNet backward is bit-reproducible)
 //   pso_im2col_conv        the 3x3 patch matrix [B*Ho*Wo][9*(C1+C2)] (tap-major, channel-minor: the NHWC weight
 //                          layout [Cout][kh][kw][Cin]) of a NORMAL (stride 1/2) or UP2 (nearest 2x upsample) conv over
 //                          one or two concatenated NHWC sources, so dW = dY^T . cols is one TN GEMM.
@@ -166,6 +168,108 @@ __global__ __launch_bounds__(256) void ln_dparam8_kernel(int M, int C, const bf1
   cs2_flush<2>(acc, dgamma, dbeta, blockIdx.x * 512, C, red);
 }
 
+// Ordered (deterministic) forms -- no float atomics: stage 1 stores every row block's column partials, stage 2 adds
+// them in row-block order (the full-UNet backward then gives the same bits run to run and in any stream schedule).
+// colsum: row block j of group g covers rows [g*rpg + j*CS2_ROWS, min(+CS2_ROWS, (g+1)*rpg)) (blocks never straddle a
+// group); part[(g*nbg + j)][N].  LN dparam: part[j][2][C] (dgamma, dbeta).  256 threads = 4 row slices x 64 chunks of 8
+// columns; the slices are folded in LDS in slice order.
+template <int NS>
+__device__ __forceinline__ void cs2_store(float (&acc)[NS][8], float* __restrict__ p0, float* __restrict__ p1, int nb,
+                                          int N, float (*red)[4][64][8]) {
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[k][ty][tx][e] = acc[k][e];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = h * 256 + t, n = nb + c;
+    if (n >= N) continue;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      (k ? p1 : p0)[n] = red[k][0][c >> 3][c & 7] + red[k][1][c >> 3][c & 7] + red[k][2][c >> 3][c & 7] +
+                         red[k][3][c >> 3][c & 7];
+  }
+}
+
+__device__ __forceinline__ void load8_tail(const bf16_t* __restrict__ p, int n, int N, float (&f)[8], bool vec) {
+  if (vec && n + 8 <= N) {
+    unpack8f(*reinterpret_cast<const uint4*>(p), f);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = n + e < N ? bf2f(p[e]) : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, const bf16_t* __restrict__ x, long ldx,
+                                                          long rpg, int nbg, int vec, float* __restrict__ part) {
+  __shared__ float red[1][4][64][8];
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+  const int n = (blockIdx.x * 64 + tx) * 8;
+  const long g = blockIdx.y / nbg, j = blockIdx.y - g * nbg;
+  const long r0 = g * rpg + j * CS2_ROWS, r1 = min(min(M, (g + 1) * rpg), r0 + CS2_ROWS);
+  float acc[1][8] = {{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+  if (n < N) {
+    for (long m = r0 + ty; m < r1; m += 4) {
+      float f[8];
+      load8_tail(x + m * ldx + n, n, N, f, vec != 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[0][e] += f[e];
+    }
+  }
+  cs2_store<1>(acc, part + (size_t)blockIdx.y * N, nullptr, blockIdx.x * 512, N, red);
+}
+
+// out[g][n] += sum_j part[g*nbg + j][n], j in order
+__global__ void colsum_reduce_kernel(int G, int nbg, int N, const float* __restrict__ part, float* __restrict__ out,
+                                     long ldo) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)G * N) return;
+  const int g = (int)(i / N), n = (int)(i - (long)g * N);
+  const float* p = part + (size_t)g * nbg * N + n;
+  float s = 0.f;
+  for (int j = 0; j < nbg; ++j) s += p[(size_t)j * N];
+  out[(long)g * ldo + n] += s;
+}
+
+__global__ __launch_bounds__(256) void ln_dparam_part_kernel(int M, int C, const bf16_t* __restrict__ x, long ldx,
+                                                             const bf16_t* __restrict__ dy, long lddy,
+                                                             const float* __restrict__ stats, int vec,
+                                                             float* __restrict__ part) {
+  __shared__ float red[2][4][64][8];
+  const int t = threadIdx.x, tx = t & 63, ty = t >> 6;
+  const int c = (blockIdx.x * 64 + tx) * 8;
+  const int r0 = blockIdx.y * CS2_ROWS, r1 = min(M, r0 + CS2_ROWS);
+  float acc[2][8] = {{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+  if (c < C) {
+    for (int m = r0 + ty; m < r1; m += 4) {
+      const float mean = stats[2 * m], rstd = stats[2 * m + 1];
+      float xs[8], ds[8];
+      load8_tail(x + (long)m * ldx + c, c, C, xs, vec != 0);
+      load8_tail(dy + (long)m * lddy + c, c, C, ds, vec != 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[0][e] += ds[e] * (xs[e] - mean) * rstd;
+        acc[1][e] += ds[e];
+      }
+    }
+  }
+  float* p = part + (size_t)blockIdx.y * 2 * C;
+  cs2_store<2>(acc, p, p + C, blockIdx.x * 512, C, red);
+}
+
+// dgamma[c] += sum_j part[j][0][c], dbeta[c] += sum_j part[j][1][c], j in order
+__global__ void ln_dparam_reduce_kernel(int nb, int C, const float* __restrict__ part, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * C) return;
+  const int k = i / C, c = i - k * C;
+  float s = 0.f;
+  for (int j = 0; j < nb; ++j) s += part[((size_t)j * 2 + k) * C + c];
+  (k ? dbeta : dgamma)[c] += s;
+}
+
 // one thread per (output pixel, tap, 8-channel chunk)
 __global__ __launch_bounds__(256) void im2col_conv_kernel(int mode, int B, const bf16_t* __restrict__ s1, int C1,
                                                           const bf16_t* __restrict__ s2, int C2, int H, int W, int Ho,
@@ -241,6 +345,49 @@ int pso_layer_norm_dparam(int M, int C, const void* x, long ldx, const void* dy,
   ln_dparam_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, stats,
                                                          dgamma, dbeta);
   return pso_check_launch("pso_layer_norm_dparam");
+}
+
+static int colsum_nbg(long M, long rpg) { return (int)(((M < rpg ? M : rpg) + CS2_ROWS - 1) / CS2_ROWS); }
+
+size_t pso_colsum_acc_ws_bytes(long M, int N, long rows_per_group) {
+  if (M <= 0 || N <= 0 || rows_per_group <= 0) return 0;
+  const long G = (M + rows_per_group - 1) / rows_per_group;
+  return (size_t)G * colsum_nbg(M, rows_per_group) * N * sizeof(float);
+}
+
+int pso_colsum_acc_ws(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* ws,
+                      size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && N > 0 && x && out && rows_per_group > 0, "pso_colsum_acc_ws: bad arguments");
+  if (M == 0) return PSO_OK;
+  PSO_ARG_CHECK(ws && ws_bytes >= pso_colsum_acc_ws_bytes(M, N, rows_per_group), "pso_colsum_acc_ws: workspace");
+  const long G = (M + rows_per_group - 1) / rows_per_group;
+  const int nbg = colsum_nbg(M, rows_per_group);
+  PSO_ARG_CHECK(G * nbg < 65536L * 1024, "pso_colsum_acc_ws: too many row blocks");
+  const int vec = (N % 8) == 0 && (((uintptr_t)x) & 15) == 0 && (ldx % 8) == 0;
+  const hipStream_t st = (hipStream_t)stream;
+  colsum_part_kernel<<<dim3((N + 511) / 512, (unsigned)(G * nbg)), 256, 0, st>>>(M, N, (const bf16_t*)x, ldx,
+                                                                                rows_per_group, nbg, vec, (float*)ws);
+  colsum_reduce_kernel<<<(unsigned)((G * N + 255) / 256), 256, 0, st>>>((int)G, nbg, N, (const float*)ws, out, ldo);
+  return pso_check_launch("pso_colsum_acc_ws");
+}
+
+size_t pso_layer_norm_dparam_ws_bytes(int M, int C) {
+  if (M <= 0 || C <= 0) return 0;
+  return (size_t)((M + CS2_ROWS - 1) / CS2_ROWS) * 2 * C * sizeof(float);
+}
+
+int pso_layer_norm_dparam_ws(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
+                             float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  PSO_ARG_CHECK(M >= 0 && C > 0 && x && dy && stats && dgamma && dbeta, "pso_layer_norm_dparam_ws: bad arguments");
+  if (M == 0) return PSO_OK;
+  PSO_ARG_CHECK(ws && ws_bytes >= pso_layer_norm_dparam_ws_bytes(M, C), "pso_layer_norm_dparam_ws: workspace");
+  const int nb = (M + CS2_ROWS - 1) / CS2_ROWS;
+  const int vec = (C % 8) == 0 && ((((uintptr_t)x) | ((uintptr_t)dy)) & 15) == 0 && (ldx % 8) == 0 && (lddy % 8) == 0;
+  const hipStream_t st = (hipStream_t)stream;
+  ln_dparam_part_kernel<<<dim3((C + 511) / 512, nb), 256, 0, st>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy,
+                                                                  lddy, stats, vec, (float*)ws);
+  ln_dparam_reduce_kernel<<<(2 * C + 255) / 256, 256, 0, st>>>(nb, C, (const float*)ws, dgamma, dbeta);
+  return pso_check_launch("pso_layer_norm_dparam_ws");
 }
 
 int pso_im2col_conv(int mode, int B, const void* src1, int C1, const void* src2, int C2, int H, int W, int Ho, int Wo,

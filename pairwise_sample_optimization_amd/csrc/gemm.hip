@@ -867,7 +867,14 @@ __global__ void gemm_splitk_reduce_kernel(GemmArgs g, int ks) {
 // caller-owned fp32 workspace (deterministic).  The partials cost 8 M N bytes per split against 2 M N K / ks flop,
 // so only K >= 2048 qualifies.  Returns ks (0: no split) and the tile.
 struct SplitPlan { int ks, bm, bn; };
+// Benchmark knobs (A/B variants, forced tiles, raster groups): only the tools build (-DPSO_BENCH_KNOBS ->
+// libpso_amd_knobs.so, include/pso_amd_knobs.h) has them as mutable state; the product library's are compile-time
+// zeros, so every knob branch folds away and the measured-not-kept forms are not compiled into it.
+#ifdef PSO_BENCH_KNOBS
 static int g_gemm_variant = 0;
+#else
+static constexpr int g_gemm_variant = 0;
+#endif
 static SplitPlan gemm_split_plan(int M, int N, int K1, int K2, bool has_tail, bool dense) {
   SplitPlan p{0, 0, 0};
   if (!dense || M <= 0 || N <= 0 || (N % 4) != 0) return p;
@@ -888,9 +895,13 @@ static SplitPlan gemm_split_plan(int M, int N, int K1, int K2, bool has_tail, bo
   return p;
 }
 
+#ifdef PSO_BENCH_KNOBS
 static int g_tn_split = 0;  // 0 = auto (benchmark knob)  // 0 auto, 1 force 256x128x3, 2 force 128x128x3, 3 force 128x128x2 (benchmarks)
-
 static int g_gemm_group = 0;  // benchmark knob: raster group rows (0 = automatic)
+#else
+static constexpr int g_tn_split = 0;
+static constexpr int g_gemm_group = 0;
+#endif
 int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced group is used as given
 // raster group rows: C2-step sweep (tools/_var_ab.sh, same box) 2 / 3 / 4 / 5 / 6 / 8 / 16 -> 240.4 / 239.7 / 239.1 /
 // 239.2 / 238.9 / 240.5 / 241.9 ms
@@ -1035,6 +1046,8 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (ok160 && gv_raw != 37 && (gv_raw == 38 || (gv == 0 && t160 >= 256 && Ktot >= 2560)))
     return pso_gemm8p160_run(g.M, g.N, g.K1, g.a1, g.lda1, g.b1, g.ldb1, g.a2, g.lda2, g.K2, g.b2, g.ldb2, g.tail_m,
                              g.tail_group_n, g.alpha, g.bias, g.resid, g.ldr, g.out, g.ldo, g.group_m, st);
+  const bool n160 = (g.N % 160) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
+#ifdef PSO_BENCH_KNOBS  // forced tile shapes (A/B and tests of the knobs build)
   if (gv == 4 && bn256_ok) return launch<256, 256, 2, 4, 2>(g, st);
   if (gv == 5 && !bn64_only) return launch<256, 128, 2, 4, 2>(g, st);
   if (gv == 1 && !bn64_only) return launch<256, 128, 4, 2, 3>(g, st);
@@ -1045,7 +1058,6 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (gv == 8 && !bn64_only) return launch<128, 128, 2, 4, 2>(g, st);
   if (gv == 10 && bn256_ok) return launch<256, 256, 2, 4, 2, true>(g, st);
   if (gv == 11 && !bn64_only) return launch<128, 128, 2, 4, 2, true>(g, st);
-  const bool n160 = (g.N % 160) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 160) == 0);
   const bool n320 = (g.N % 320) == 0 && (g.tail_group_n == 0 || (g.tail_group_n % 320) == 0);
   if (gv == 12 && n160) return launch<128, 160, 2, 2, 2>(g, st);
   if (gv == 14 && n160) return launch<256, 160, 2, 2, 2>(g, st);
@@ -1065,6 +1077,7 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   if (gv == 27 && !bn64_only) return launch<64, 128, 2, 2, 4>(g, st);
   if (gv == 28 && !bn64_only) return launch<128, 128, 2, 4, 4>(g, st);
   if (gv == 29 && !bn64_only) return launch<64, 64, 2, 2, 5>(g, st);
+#endif
   // Tile choice by occupancy (~2 co-resident 4-wave blocks per CU, 256 CUs): large grids keep 128x128 (best operand
   // reuse); grids that would leave CUs idle drop to 64x128 / 128x64 / 64x64 (e.g. the L2 projections, M=4096 N=1280,
   // and the skinny LoRA projections N = r..3r).
@@ -1097,9 +1110,11 @@ static int run_gemm(GemmArgs& g, hipStream_t st) {
   // a workspace, pso_gemm_ws): variant 49 takes the register-pipelined 8-wave 128 x 128 tiles. They win in isolation
   // (tools/small_m_bench.py: 2048 x 1280 x 1280 + LoRA 404 vs 319 TF/s) but lose inside the bs = 1 step
   // (tools/shape_prof.py, one box: 252-256 vs 277 TF/s), so 64 x 64 stays the default there
+#ifdef PSO_BENCH_KNOBS
   if (gv_raw == 49 && !g.conv.mode && !bn64_only && (g.N % 128) == 0 && tiles(64, 160) <= 256 &&
       tiles(128, 128) >= 128 && tiles(128, 160) < 256)
     return launch<128, 128, 2, 4, 2, true>(g, st);
+#endif
   if (n160 && tiles(128, 160) >= 256) return launch<128, 160, 2, 2, 2>(g, st);
   if (bn256_ok && (g.N % 256) == 0 && tiles(256, 256) >= (g.conv.mode ? 128 : 256))
     return launch<256, 256, 2, 4, 2>(g, st);
@@ -1827,11 +1842,12 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   if (g_gemm_variant != 31 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw))
     return pso_gemm8p_run(1, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, bias, nullptr, 0, out, ldo,
                           out_pre, ld_pre, g.tail_m, nullptr, 0, g.group_m, (hipStream_t)stream);
-  // tile A/B knobs (64-column wave tiles are what the interleaved epilogue needs)
+#ifdef PSO_BENCH_KNOBS  // tile A/B knobs (64-column wave tiles are what the interleaved epilogue needs)
   if (g_gemm_variant == 33) return launch<128, 128, 2, 2, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
   if (g_gemm_variant == 34) return launch<128, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
   if (g_gemm_variant == 35) return launch<256, 128, 4, 2, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
   if (g_gemm_variant == 36) return launch<128, 128, 2, 2, 3, false, EPI_GEGLU>(g, (hipStream_t)stream);
+#endif
   return launch<256, 256, 2, 4, 2, false, EPI_GEGLU>(g, (hipStream_t)stream);
 }
 
@@ -1870,10 +1886,12 @@ int pso_gemm_geglu_bwd(int M, int N, const void* a, long lda, int K, const void*
   return launch<64, 64, 2, 2, 2, false, EPI_GEGLU_BWD>(g, st);
 }
 
+#ifdef PSO_BENCH_KNOBS
 void pso_gemm_set_variant(int v) {
   g_gemm_variant = v % 100;
   g_gemm_group = v / 100;
 }
+#endif
 
 int pso_gemm_skinny_grouped(int M, int N, int K, const void* A, long lda, const void* W, long ldw, float alpha,
                             void* out, long ldo, int groups, void* stream) {
@@ -1888,7 +1906,9 @@ int pso_gemm_tn(int M, int I, int J, const void* A, long lda, const void* B, lon
                 long ldo, void* stream) {
   return pso_gemm_tn_grouped(M, I, J, A, lda, B, ldb, alpha, out, ldo, 0, stream);
 }
+#ifdef PSO_BENCH_KNOBS
 void pso_gemm_tn_set_split(int ks) { g_tn_split = ks; }
+#endif
 
 int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void* B, long ldb, float alpha, float* out,
                         long ldo, int group, void* stream) {
@@ -1914,10 +1934,14 @@ int pso_gemm_tn_grouped(int M, int I, int J, const void* A, long lda, const void
   }
   // full-weight gradients (both sides >= 128 wide): 128 x 128 tiles; split over M only as far as needed to cover ~2
   // rounds of co-resident blocks (each split adds its tile of f32 atomics)
+#ifdef PSO_BENCH_KNOBS
   static const int tn128 = [] {
     const char* e = getenv("PSO_TN128");  // benchmark knob: 0 keeps the 64 x 64 kernel everywhere
     return e ? atoi(e) : 1;
   }();
+#else
+  constexpr int tn128 = 1;
+#endif
   const int t128 = ((I + 127) / 128) * ((J + 127) / 128);
   if (tn128 && g_tn_split == 0 && I >= 128 && J >= 128 && (long)M * lda < (1L << 30) && (long)M * ldb < (1L << 30)) {
     // split over M only while its f32 atomics stay small next to the product: each split adds I*J*4 bytes at the

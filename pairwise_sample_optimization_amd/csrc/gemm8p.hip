@@ -862,11 +862,15 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
 }
 
 // persistent grid: one workgroup per CU (256 on MI355X; a multiple of 8 keeps every tile of a workgroup on its XCD)
-// (benchmark knob PSO_GEMM8_GRID: a larger value = one workgroup per tile)
+// (benchmark knob PSO_GEMM8_GRID, tools build only: a larger value = one workgroup per tile)
+#ifdef PSO_BENCH_KNOBS
 static const int g_grid8 = [] {
   const char* e = getenv("PSO_GEMM8_GRID");
   return e ? atoi(e) : 256;
 }();
+#else
+static constexpr int g_grid8 = 256;
+#endif
 
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256, bool CONV = false>
 int launch8(const Gemm8Args& g, hipStream_t st) {
@@ -900,23 +904,32 @@ int launch8(const Gemm8Args& g, hipStream_t st) {
 
 template <int EPI>
 int launch8s(const Gemm8Args& g, hipStream_t st, int mode) {
+#ifdef PSO_BENCH_KNOBS
   switch (mode & 3) {
     case 0: return launch8<EPI, true, false>(g, st);
     case 1: return launch8<EPI, false, false>(g, st);
     case 2: return launch8<EPI, true, true>(g, st);
     default: return launch8<EPI, false, true>(g, st);
   }
+#else
+  (void)mode;
+  return launch8<EPI, true, false>(g, st);
+#endif
 }
 
 }  // namespace
 
 // Host entries used by gemm.hip (preconditions checked there): N % 256 == 0, K % 64 == 0, 16-B aligned rows, every
 // operand's M * ld (or N * ld) below 2^30 elements (byte offsets of the buffer loads are 32-bit).
+#ifdef PSO_BENCH_KNOBS
 static int g_skip_epi8 = 0;
 // benchmark knobs, bit 1: wave groups in lockstep (default: staggered by half a phase, +10-18 % on every UNet shape,
 // tools/gemm8_ab.py); bit 2: static priority for waves 4-7
 static int g_mode8 = 0;
 extern "C" void pso_gemm8p_skip_epilogue(int on) { g_skip_epi8 = on & 1; g_mode8 = (on >> 1) & 3; }
+#else
+static constexpr int g_skip_epi8 = 0, g_mode8 = 0;
+#endif
 
 int pso_gemm8p_run(int epi, int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* a2,
                    long lda2, int K2, const void* w2, long ldw2, int tail_m, int tail_group_n, float alpha,

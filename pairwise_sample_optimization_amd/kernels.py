@@ -747,19 +747,26 @@ def axpby(a, x, b=0.0, z=None, out=None):
 
 
 def colsum_acc(x, out, rows_per_group=None):
-    """out [G, N] f32 += per-group column sums of x [M, N] bf16 (G = M / rows_per_group; bias / row-bias grads)."""
+    """out [G, N] f32 += per-group column sums of x [M, N] bf16 (G = M / rows_per_group; bias / row-bias grads), in a
+    fixed summation order (pso_colsum_acc_ws: per-row-block partials through a workspace, no float atomics)."""
     M, N = x.shape
     rpg = M if rows_per_group is None else rows_per_group
-    check(lib().pso_colsum_acc(M, N, ptr(x), _row_stride(x), rpg, ptr(out), out.stride(0) if out.dim() > 1 else N,
-                               stream_ptr()), "pso_colsum_acc")
+    wsb = int(lib().pso_colsum_acc_ws_bytes(M, N, rpg))
+    ws = torch.empty(max(wsb, 16), device=x.device, dtype=torch.uint8)
+    check(lib().pso_colsum_acc_ws(M, N, ptr(x), _row_stride(x), rpg, ptr(out), out.stride(0) if out.dim() > 1 else N,
+                                  ptr(ws), ws.numel(), stream_ptr()), "pso_colsum_acc_ws")
     return out
 
 
 def layer_norm_dparam(x, dy, stats, dgamma, dbeta):
-    """dgamma / dbeta [C] f32 += LayerNorm weight / bias grads (stats from layer_norm_fwd)."""
+    """dgamma / dbeta [C] f32 += LayerNorm weight / bias grads (stats from layer_norm_fwd), in a fixed summation order
+    (pso_layer_norm_dparam_ws)."""
     M, C = x.shape
-    check(lib().pso_layer_norm_dparam(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats),
-                                      ptr(dgamma), ptr(dbeta), stream_ptr()), "pso_layer_norm_dparam")
+    wsb = int(lib().pso_layer_norm_dparam_ws_bytes(M, C))
+    ws = torch.empty(max(wsb, 16), device=x.device, dtype=torch.uint8)
+    check(lib().pso_layer_norm_dparam_ws(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats),
+                                         ptr(dgamma), ptr(dbeta), ptr(ws), ws.numel(), stream_ptr()),
+          "pso_layer_norm_dparam_ws")
 
 
 def im2col_conv(x, x2=None, mode=CONV_NORMAL, stride=1, pad=1, out_hw=None):

@@ -149,6 +149,11 @@ def main_full(args):
     fg.grad.zero_()
     tr.micro_step(mb)
     local = fg.grad.clone()
+    fg.grad.zero_()
+    tr.n_micro = 0
+    tr.micro_step(mb)
+    local_repeat = torch.equal(fg.grad, local)  # every gradient sum of the full-UNet backward is ordered
+    fg.grad.copy_(local)
     for b in range(len(tr.buckets.buckets)):
         assert tr.buckets.works[b] is None
     tr.buckets.finish()  # issues every bucket of the local gradient, waits, casts the bf16 wire back
@@ -175,6 +180,7 @@ def main_full(args):
                    "wire": str(tr.allreduce_dtype), "scale": scale, "loss": loss.item(),
                    "numel": fg.grad.numel(), "bucketed_equals_flat": torch.equal(gc_, gb),
                    "overlapped_vs_flat_rel": ((ga - gb).norm() / gb.norm()).item(),
+                   "overlapped_equals_flat": torch.equal(ga, gb), "local_run_to_run_equal": local_repeat,
                    "synced_equal_across_ranks": ranks_equal,
                    "masters_equal_across_ranks": all(torch.equal(mg[0], x) for x in mg),
                    "work_equal_across_ranks": all(torch.equal(wk[0], x) for x in wk),

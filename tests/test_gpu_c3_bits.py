@@ -77,3 +77,47 @@ def test_full_policy_and_frozen_reference_same_bits(cuda, B):
     assert torch.equal(e_pol_ns, e_ref)
     assert torch.equal(e_pol, e_ref)
     del rt
+
+
+def test_full_unet_micro_step_run_to_run_bits(cuda):
+    """C3 at 1024^2 (DMD2, N = 4 -> T = 3, 1 pair: 6 images in one pass, full-UNet grads against a frozen reference
+    UNet, D:777-864): two micro-steps on the same window give the same loss and the same gradient of all 1,680 UNet
+    parameters bit for bit.  Every sum of the full-UNet backward is ordered -- bias / LayerNorm / GroupNorm parameter
+    sums through row-block partials (pso_colsum_acc_ws, pso_layer_norm_dparam_ws, the GroupNorm split dparam), the
+    weight-gradient TN products through split workspaces -- and the side-stream weight-gradient launches race nothing."""
+    from pairwise_sample_optimization_amd.trainer import PSOTrainer, compute_time_ids
+    from pairwise_sample_optimization_amd.unet import UNetConfig
+    cfg = UNetConfig.sdxl(128)
+    unet, ref_unet = _make(cuda, cfg), _make(cuda, cfg)
+    fg = unet.enable_full_grads()
+    ref_unet.prepare()
+    unet.prepare()
+    with torch.no_grad():  # policy != reference (as after some updates): a 3 % weight perturbation
+        gp = torch.Generator(device="cuda").manual_seed(7)
+        for p in unet.parameters():
+            p.add_((torch.randn(p.shape, device=cuda, generator=gp) * 3e-2 * p.float().abs().mean()).bfloat16())
+        fg.master_from_params()
+    unet.prepare()
+    tr = PSOTrainer(unet, mode="dmd", num_steps=4, gradient_accumulation_steps=1, train_batch_size=1,
+                    ref_unet=ref_unet)
+    tr.auto_step = False
+    g = torch.Generator(device="cuda").manual_seed(2000)
+    enc = torch.randn(1, 77, 2048, device=cuda, generator=g).bfloat16()
+    pooled = torch.randn(1, 1280, device=cuda, generator=g).bfloat16()
+    tid = compute_time_ids(1024, 0, cuda).repeat(1, 1)
+    buf = tr.sample_pairs(enc, pooled, tid, 128, generator=g,
+                          reward_fn=lambda img: torch.rand(img.shape[0], device=cuda, generator=g))
+    sb = tr.shuffle(buf, generator=g)
+    mb = tr.micro_batch(sb, 0, sb.n_micro)
+    grads, losses = [], []
+    for _ in range(2):
+        fg.grad.zero_()
+        tr.n_micro = 0
+        losses.append(tr.micro_step(mb).item())
+        torch.cuda.synchronize()
+        grads.append(fg.grad.clone())
+    nz = (grads[0] != 0).sum().item()
+    diff = (grads[0] != grads[1]).sum().item()
+    print(f"C3 run-to-run: losses {losses}; gradient elements differing {diff} of {grads[0].numel()} ({nz} non-zero)")
+    assert nz > grads[0].numel() // 2
+    assert losses[0] == losses[1] and diff == 0

@@ -595,6 +595,20 @@ def test_fullgrad_helpers(cuda):
     y = F.layer_norm(xl.float(), (C,), w, b, 1e-5)
     gw, gb = torch.autograd.grad(y, (w, b), dy.float())
     assert _rel(dg, gw) < 1e-4 and _rel(db, gb) < 1e-5
+    # the ordered forms are bit-reproducible (no float atomics): twice the same bits; N = 4 (conv_out's bias), groups
+    # of 1000 rows (row blocks end at every group edge)
+    for N_, rpg in ((4, None), (1280, 1000), (320, 4096)):
+        xr = torch.randn(4000 if rpg != 4096 else 8192, N_, device=cuda, generator=g).bfloat16()
+        G_ = 1 if rpg is None else (xr.shape[0] + rpg - 1) // rpg
+        o1, o2 = torch.zeros(G_, N_, device=cuda), torch.zeros(G_, N_, device=cuda)
+        K_.colsum_acc(xr, o1, rows_per_group=rpg)
+        K_.colsum_acc(xr, o2, rows_per_group=rpg)
+        r_ = rpg or xr.shape[0]
+        want = torch.stack([xr[i * r_:(i + 1) * r_].float().sum(0) for i in range(G_)])
+        assert torch.equal(o1, o2) and _rel(o1, want) < 1e-5, (N_, rpg)
+    dg2, db2 = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    K_.layer_norm_dparam(xl, dy, st, dg2, db2)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
     for mode, stride, C1, C2 in [(K_.CONV_NORMAL, 1, 64, 0), (K_.CONV_NORMAL, 2, 32, 0), (K_.CONV_UP2, 1, 32, 0),
                                  (K_.CONV_NORMAL, 1, 64, 32)]:
         B, H, W = 2, 9, 7
