@@ -482,6 +482,8 @@ def spawn_ranks(n):
 
 def main():
     args = parse()
+    if os.environ.get("PSO_BENCH_GEMM_VARIANT") or os.environ.get("PSO_BENCH_ATTN_VARIANT"):
+        os.environ["PSO_LIB"] = "knobs"  # A/B knobs exist in the tools build only (include/pso_amd_knobs.h)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

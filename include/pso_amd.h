@@ -146,16 +146,8 @@ int pso_gemm_batched(int batch, int M, int N, int K, const void* a, long lda, lo
  * "gemm_bf16_kernel<128, 160, 0, 2, 2, 2, false, 0>"): lets the bench attribute its HIP-event timings per kernel. */
 const char* pso_last_kernel(void);
 
-/* Tile-configuration override for benchmarks: 0 = automatic per shape, 1 = 256x128 (8 waves, 3-stage),
- * 2 = 128x128 (4 waves, 3-stage), 3 = 128x128 (4 waves, 2-stage), 4 = 256x256 (8 waves), 5 = 256x128 (8 waves),
- * 6 = 64x128 (4 waves), 7 = 128x256 (8 waves), 8 = 128x128 (8 waves). */
-void pso_gemm_set_variant(int v);
-/* Benchmark knob of the 8-phase 256x256 kernel: 1 = keep the accumulators live but store nothing (main-loop cost). */
-void pso_gemm8p_skip_epilogue(int on);
-/* Benchmark knob: split count of pso_gemm_tn over the reduction rows (0 = automatic). */
-void pso_gemm_tn_set_split(int ks);
-/* benchmark knob: attention forward tile (0 = auto, 2 = 128 / 4 = 256 queries per workgroup) */
-void pso_attention_set_variant(int v);
+/* (The benchmark knobs -- forced tile shapes, A/B variants -- are not part of this library: they live in the tools
+ * build libpso_amd_knobs.so, declared in include/pso_amd_knobs.h.  This library holds no mutable global state.) */
 
 /* TN GEMM, f32 accumulate: out[I][J] += alpha * sum_m A[m][I] * B[m][J] (A [M][I], B [M][J] row-major, row strides
  * lda/ldb; I, J multiples of 8).  Replaces the peft LoRA weight-gradient GEMMs of the backward (dA = v^T x,

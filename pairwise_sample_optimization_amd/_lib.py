@@ -10,7 +10,11 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PSO_LIB_PATH") or os.path.join(_HERE, "libpso_amd.so")  # override: same-box A/B only
+# PSO_LIB=knobs selects the TOOLS build (libpso_amd_knobs.so: the same sources with the benchmark knobs of
+# include/pso_amd_knobs.h compiled in) for A/B measurements and the knob-pinned kernel-form tests; the product path
+# and everything else load libpso_amd.so, which has no knobs.  PSO_LIB_PATH: an explicit file (same-box A/B only).
+KNOBS = os.environ.get("PSO_LIB", "") == "knobs"
+LIB_PATH = os.environ.get("PSO_LIB_PATH") or os.path.join(_HERE, "libpso_amd_knobs.so" if KNOBS else "libpso_amd.so")
 
 PSO_F32 = 0
 PSO_BF16 = 1
@@ -55,7 +59,6 @@ SIGNATURES = {
     "pso_gemm_ws": (ci, [ci, ci, vp, cl, ci, vp, cl, vp, cl, ci, vp, cl, cf, vp, vp, cl, ci, vp, cl, vp, cl, ci, ci,
                          ci, ci, vp, csz, vp]),
     "pso_gemm_batched": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, cf, vp, cl, cl, ci, vp]),
-    "pso_gemm_set_variant": (None, [ci]),
     "pso_last_kernel": (ctypes.c_char_p, []),
     "pso_attention_small": (ci, [ci, ci, ci, ci, vp, cl, cl, vp, cl, cl, vp, cl, cl, ci, cf, vp, cl, cl, vp]),
     "pso_activation": (ci, [cl, vp, ci, vp]),
@@ -66,9 +69,6 @@ SIGNATURES = {
     "pso_patchify": (ci, [ci, ci, ci, ci, ci, vp, vp, vp]),
     "pso_clip_preprocess_ws_bytes": (csz, [ci, ci, ci, ci]),
     "pso_clip_preprocess": (ci, [ci, ci, ci, vp, ci, ci, ci, ci, vp, vp, vp, vp, csz, vp]),
-    "pso_gemm8p_skip_epilogue": (None, [ci]),
-    "pso_gemm_tn_set_split": (None, [ci]),
-    "pso_attention_set_variant": (None, [ci]),
     "pso_gemm_tn": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
     "pso_gemm_tn_grouped": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, ci, vp]),
     "pso_gemm_tn_geglu": (ci, [ci, ci, ci, vp, cl, vp, cl, cf, vp, cl, vp]),
@@ -139,6 +139,16 @@ SIGNATURES = {
 }
 
 
+# include/pso_amd_knobs.h: bound only when the TOOLS build is loaded (PSO_LIB=knobs)
+KNOB_SIGNATURES = {
+    "pso_gemm_set_variant": (None, [ci]),
+    "pso_gemm8p_skip_epilogue": (None, [ci]),
+    "pso_gemm_tn_set_split": (None, [ci]),
+    "pso_attention_set_variant": (None, [ci]),
+    "pso_attn_pp_trace": (ci, [vp]),
+}
+
+
 class PsoLibError(RuntimeError):
     pass
 
@@ -148,6 +158,18 @@ def _bind(lib):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if KNOBS:
+        for name, (res, args) in KNOB_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+
+
+def require_knobs(what):
+    """The benchmark knobs exist in the TOOLS build only (include/pso_amd_knobs.h)."""
+    if not KNOBS:
+        raise PsoLibError(f"{what} is a benchmark knob: run with PSO_LIB=knobs (libpso_amd_knobs.so); the product "
+                          "library libpso_amd.so has none")
 
 
 def lib():

@@ -893,7 +893,9 @@ __device__ __forceinline__ void pin_segment<4, 2>(f32x4 (&x)[4][2], f32x4 (&y)[4
 __device__ __forceinline__ void pp_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // PRIO: the A segment at s_setprio 1.  TR (diagnostic): workgroup 0's waves 0 and 4 record the shader clock before
-// and after every barrier in g_pp_trace (tools/pp_trace.py)
+// and after every barrier in g_pp_trace (tools/pp_trace.py).  Measured, not the default: compiled
+// into the tools build only (-DPSO_BENCH_KNOBS).
+#ifdef PSO_BENCH_KNOBS
 __device__ unsigned long long g_pp_trace[2][520];
 template <int STG, bool PRIO = false, bool TR = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkv_pp_kernel(AttnArgs a, int nkb) {
@@ -1139,6 +1141,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv_pp_kernel(AttnArgs a, int
     }
   }
 }
+#endif  // PSO_BENCH_KNOBS (the ping-pong dK/dV form)
 
 // ================================================================================================================
 // backward dQ: forward structure (128 queries per workgroup, S^T = K.Q^T lane-local per query), K/V tiles through LDS;
@@ -1369,15 +1372,21 @@ static int cross_qsplit(int B, int H, int Sq, int Sk) {
   return qs < 1 ? 1 : qs;
 }
 
+// benchmark knobs (tools build only; compile-time zeros in the product library, whose dispatch is the default forms)
+#ifdef PSO_BENCH_KNOBS
 static int g_attn_fwd_variant = 0;
 static bool g_attn_vsum = false;
 static int g_attn_bwd_variant = 0;  // benchmark knob (the tens digit of pso_attention_set_variant): see pso_attention_bwd
 static bool g_attn_pp_trace = false;  // the ping-pong dK/dV form records segment clocks (diagnostic)
+#else
+static constexpr int g_attn_fwd_variant = 0, g_attn_bwd_variant = 0;
+#endif
 
 static bool a16(const void* p, long ld) { return (((uintptr_t)p) & 15) == 0 && (ld % 8) == 0; }
 
 extern "C" {
 
+#ifdef PSO_BENCH_KNOBS
 // diagnostic: the segment-start clocks of the last traced ping-pong dK/dV launch (2 x 520, group-major)
 int pso_attn_pp_trace(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_trace), sizeof(g_pp_trace)) == hipSuccess ? 0 : 1;
@@ -1389,6 +1398,7 @@ void pso_attention_set_variant(int v) {
   g_attn_vsum = (v / 100) % 10 == 1;  // 100+: row sums on the VALU (A/B knob)
   g_attn_pp_trace = (v / 1000) % 10 == 1;
 }
+#endif
 
 int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
                       long sk_b, const void* v, long ldv, long sv_b, float scale, void* o, long ldo, long so_b,
@@ -1412,16 +1422,22 @@ int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   const int qsel = fv >= 5 ? fv - 5 : fv;
   const bool big = qsel == 4 || ((qsel == 0 || qsel == 1) && (long)nq4 * H * B >= 1024 && Sk > 128);
   hipStream_t st = (hipStream_t)stream;
+#ifdef PSO_BENCH_KNOBS
   if (g_attn_vsum) {
     if (big) attn_fwd_kernel<4, false><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
     else attn_fwd_kernel<2, false><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
+    return pso_check_launch("pso_attention_fwd");
   } else if (fv >= 5) {
     if (big) attn_fwd_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
     else attn_fwd_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
+    return pso_check_launch("pso_attention_fwd");
   } else if (fv == 1) {  // lane-local growth test (LG)
     if (big) attn_fwd2_kernel<4, true><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
     else attn_fwd2_kernel<2, true><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
-  } else if (big) {
+    return pso_check_launch("pso_attention_fwd");
+  }
+#endif
+  if (big) {
     attn_fwd2_kernel<4><<<nq4 * H * B, ATT_THREADS, 0, st>>>(a, nq4);
   } else {
     attn_fwd2_kernel<2><<<nq2 * H * B, ATT_THREADS, 0, st>>>(a, nq2);
@@ -1474,8 +1490,9 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // one LDS image per operand (ONE) by default: bit-identical to the two-image form (bwd variant 3, A/B knob) and
   // 3-5 % faster on the self-attention shapes (L1 1.113 vs 1.157 ms, L2 0.168 vs 0.177 ms, medians of 4 alternated
   // runs, profiles/r05_attn_bwd_ab.log); 5 / 6 = ONE with rings of 3 / 4 (no faster)
-  const int bv = g_attn_bwd_variant;
   const dim3 gq(cdiv(Sq, 128), H, B);
+#ifdef PSO_BENCH_KNOBS
+  const int bv = g_attn_bwd_variant;
   if (bv == 3 || bv == 1) attn_bwd_dq_kernel<3, false><<<gq, ATT_THREADS, 0, st>>>(a);
   else if (bv == 6) attn_bwd_dq_kernel<4, true><<<gq, ATT_THREADS, 0, st>>>(a);
   else attn_bwd_dq_kernel<3, true><<<gq, ATT_THREADS, 0, st>>>(a);
@@ -1532,6 +1549,13 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
     const size_t shm = 2 * (4 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
     attn_bwd_dkv_kernel<2, 2, true><<<nkb * qsplit * H * B, ATT_THREADS, shm, st>>>(a, nkb);
   }
+#else
+  attn_bwd_dq_kernel<3, true><<<gq, ATT_THREADS, 0, st>>>(a);
+  {  // ONE: Q / dO once per stage (swz_tr image for row and transposed reads), 2-stage ring
+    const size_t shm = 2 * (2 * ATT_KT * ATT_D * sizeof(bf16_t) + 2 * 64 * sizeof(float));
+    attn_bwd_dkv_kernel<2, 2, true, true><<<dim3(nkb * qsplit * H * B), ATT_THREADS, shm, st>>>(a, nkb);
+  }
+#endif
   if (qsplit > 1) {
     // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)
     const long rows = (long)B * Sk;

@@ -5,6 +5,9 @@
 #include <stddef.h>
 
 #include "../../include/pso_amd.h"
+#ifdef PSO_BENCH_KNOBS
+#include "../../include/pso_amd_knobs.h"
+#endif
 
 typedef uint16_t bf16_t;  // raw bf16 storage
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -107,8 +107,9 @@ __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_nt_kernel(int M, int N,
   }
 }
 
-// benchmark knob (PSO_SKINNY_VARIANT): 1 = 16-row tiles x 8 K steps in flight, 2 = 32-row x 8, 3 = 16-row x 4,
-// 4 = never 5 steps (the K = 1280 single-round form off)
+// benchmark knob (PSO_SKINNY_VARIANT, tools build only): 1 = 16-row tiles x 8 K steps in flight, 2 = 32-row x 8,
+// 3 = 16-row x 4, 4 = never 5 steps (the K = 1280 single-round form off)
+#ifdef PSO_BENCH_KNOBS
 static int skinny_variant() {
   static int v = -1;
   if (v < 0) {
@@ -117,11 +118,15 @@ static int skinny_variant() {
   }
   return v;
 }
+#else
+static constexpr int skinny_variant() { return 0; }
+#endif
 
 template <int NJ>
 int launch_skinny(int M, int N, int K, const bf16_t* a, long lda, const bf16_t* w, long ldw, float alpha, void* out,
                   long ldo, int out_f32, int accumulate, int groups, hipStream_t st) {
   const int var = NJ <= 2 ? skinny_variant() : 0;
+#ifdef PSO_BENCH_KNOBS
   if (var == 1 || var == 3) {
     const dim3 grid((M + 15) / 16, groups);
     if (var == 1) {
@@ -142,6 +147,7 @@ int launch_skinny(int M, int N, int K, const bf16_t* a, long lda, const bf16_t* 
                                                                 accumulate);
     return pso_check_launch("pso_gemm(skinny)");
   }
+#endif
   // K = 1280 is 40 steps of 32: with 4 steps in flight per wave that is two dependent load rounds (the second one
   // step deep); 5 steps per wave take it in one (same per-wave step order, so the same bits).  var 4 keeps the 4.
   // Up to 96 outputs (the fused q/k/v LoRA-down) for 16- and 32-row tiles, up to 32 for 64-row tiles (wider forms

@@ -419,20 +419,29 @@ static int adam8_launch(long n, int nblk, float* param, void* param_bf16, float*
   const float step_size = (-lr) * c2 / c1;
   const float decay = (float)(1.0 - (double)lr * weight_decay);
   if (nblk <= 0) return PSO_OK;
-  // element layout inside a block: PSO_ADAM8_LAYOUT (0 / 1) for the benchmark
+  // element layout inside a block: PSO_ADAM8_LAYOUT (0 / 1) for the benchmark (tools build only)
+#ifdef PSO_BENCH_KNOBS
   static const int lay = [] {
     const char* e = getenv("PSO_ADAM8_LAYOUT");
     return e ? (atoi(e) != 0) : ADAM8_LAYOUT_DEFAULT;
   }();
+#else
+  constexpr int lay = ADAM8_LAYOUT_DEFAULT;
+#endif
   const hipStream_t st = (hipStream_t)stream;
   const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2);
 #define PSO_ADAM8_ARGS                                                                                                   \
   n, param, grad, exp_avg_q, exp_avg_sq_q, absmax_m, absmax_v, beta1, omb1, beta2, omb2, c2 * eps, step_size, decay,     \
       grad_scale, clip_coef, (bf16_t*)param_bf16, desc, m32, v32, zero_grad, maps
+#ifdef PSO_BENCH_KNOBS
   if (lay)
     adamw8bit_kernel<1><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
   else
     adamw8bit_kernel<0><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
+#else
+  (void)lay;
+  adamw8bit_kernel<ADAM8_LAYOUT_DEFAULT><<<nblk, 256, 0, st>>>(PSO_ADAM8_ARGS);
+#endif
 #undef PSO_ADAM8_ARGS
   return pso_check_launch("pso_adamw8bit_step");
 }

@@ -92,8 +92,12 @@ _GEMM_WS = {}  # (M, N, K1, K2) -> pso_gemm_ws_bytes of the current dispatch var
 
 
 def gemm_set_variant(v):
-    """pso_gemm_set_variant (A/B knob of the GEMM dispatch) + a flush of the workspace-size cache: the split-K plan,
-    and so the workspace a product needs, depends on the variant."""
+    """pso_gemm_set_variant (A/B knob of the GEMM dispatch, TOOLS build only: PSO_LIB=knobs) + a flush of the
+    workspace-size cache: the split-K plan, and so the workspace a product needs, depends on the variant.
+    Variant 0 is the automatic dispatch, which the product library always runs: a no-op there."""
+    if not _lib.KNOBS and int(v) == 0:
+        return
+    _lib.require_knobs("pso_gemm_set_variant")
     lib().pso_gemm_set_variant(int(v))
     _GEMM_WS.clear()
 

@@ -1,6 +1,7 @@
 """CPU checks of the C-ABI boundary: the library builds/loads and exports every symbol include/pso_amd.h declares
 (no compute calls: there is no GPU here)."""
 import os
+import glob
 import re
 import subprocess
 
@@ -48,3 +49,31 @@ def test_no_cpu_fallback():
     a = torch.zeros(8, 8, dtype=torch.bfloat16)
     with pytest.raises(_lib.PsoLibError):
         kernels.gemm(a, a)
+
+
+def test_product_library_has_no_benchmark_knobs():
+    """the benchmark knobs (include/pso_amd_knobs.h) and the measured-not-kept kernel forms live in the
+    tools build only.  The product library exports none of the knob setters, reads no environment variable, and holds
+    no g_* dispatch state; the tools build exports every knob the header declares."""
+    from pairwise_sample_optimization_amd import _lib
+    prod = os.path.join(os.path.dirname(_lib.__file__), "libpso_amd.so")
+    knobs = os.path.join(os.path.dirname(_lib.__file__), "libpso_amd_knobs.so")
+    h = open(os.path.join(ROOT, "include", "pso_amd_knobs.h")).read()
+    h = re.sub(r"/\*.*?\*/", "", h, flags=re.S)
+    knob_names = sorted(set(re.findall(r"^\s*\w+\s+\**(pso_\w+)\(", h, flags=re.M)))
+    assert set(knob_names) == set(_lib.KNOB_SIGNATURES), knob_names
+    exported = set(re.findall(r" T (pso_\w+)", subprocess.check_output(["nm", "-D", "--defined-only", prod]).decode()))
+    assert not (exported & set(knob_names)), exported & set(knob_names)
+    undefined = subprocess.check_output(["nm", "-D", "--undefined-only", prod]).decode()
+    assert "getenv" not in undefined
+    local = subprocess.check_output(["nm", "-C", prod]).decode()
+    assert not re.search(r" [bBdD] g_(gemm|tn|attn|skip|mode|grid)", local)
+    assert "attn_bwd_dkv_pp_kernel" not in local
+    kexp = set(re.findall(r" T (pso_\w+)", subprocess.check_output(["nm", "-D", "--defined-only", knobs]).decode()))
+    assert set(knob_names) <= kexp and set(_declared()) <= kexp
+    for src in glob.glob(os.path.join(ROOT, "pairwise_sample_optimization_amd", "csrc", "*.hip")):
+        txt = open(src).read()
+        for m in re.finditer(r"^static (?:const )?(?:int|bool) g_\w+", txt, flags=re.M):
+            # every mutable dispatch global sits inside an #ifdef PSO_BENCH_KNOBS block
+            before = txt[:m.start()]
+            assert before.rfind("#ifdef PSO_BENCH_KNOBS") > before.rfind("#endif"), (src, m.group(0))

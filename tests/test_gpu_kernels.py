@@ -1,6 +1,8 @@
 """GPU parity of the GEMM / conv kernels against a plain torch fp32 reference of the same op."""
 import pytest
 import torch
+
+from pairwise_sample_optimization_amd import _lib
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
@@ -96,6 +98,7 @@ def test_conv_normal(cuda, B, C1, C2, H, Cout, ks, stride):
 
 
 @pytest.mark.parametrize("C1,C2,Cout", [(1280, 0, 1280), (1280, 640, 640)])
+@pytest.mark.knobs
 def test_conv_splitk_workspace(cuda, C1, C2, Cout):
     """The bs = 1 backward's input-gradient convolutions (2 images at 32 x 32, K = 9 * 1920 / 11520): few output
     tiles, long reduction -> pso_conv2d_ws (K-splits stored, added in split order, bias / time-embedding / residual
@@ -117,12 +120,13 @@ def test_conv_splitk_workspace(cuda, C1, C2, Cout):
     ob2 = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
     assert torch.equal(ob, ob2)
     assert _rel(_nchw(ob), ref + _nchw(res.float())) < 4e-3
-    K_.gemm_set_variant(52)
-    try:
-        on = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
-    finally:
-        K_.gemm_set_variant(0)
-    assert _rel(ob, on) < 4e-3
+    if _lib.KNOBS:  # the unsplit kernel, forced through the tools build's knob (tests/test_knobs_build.py)
+        K_.gemm_set_variant(52)
+        try:
+            on = K_.conv2d(x1, _nhwc(w), x2=x2, bias=bias, rowbias=temb, resid=res)
+        finally:
+            K_.gemm_set_variant(0)
+        assert _rel(ob, on) < 4e-3
 
 
 def test_conv_up2(cuda):
@@ -247,8 +251,9 @@ def test_gemm_splitk_accumulate(cuda, M, N, K):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 20, 21, 22, 30, 31, 37,
-                                     38, 41, 48, 49])
+@pytest.mark.knobs
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
+                                     26, 27, 28, 29, 30, 31, 37, 38, 41, 48, 49, 55])
 @pytest.mark.parametrize("M,N,K,tail", [(16384, 1920, 640, 640), (4096, 3840, 1280, 1280), (4096, 1280, 5120, 0),
                                         (8192, 640, 320, 0), (1000, 700, 136, 0), (2048, 1280, 1280, 1280)])
 def test_gemm_every_variant_large(cuda, variant, M, N, K, tail):
@@ -322,6 +327,7 @@ def test_gemm_splitk_workspace(cuda, M, N, K, K2, tail_rows, f32):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("M,N,K", [(4096, 2560, 1280), (1000, 768, 640), (300, 256, 128), (16384, 1024, 256),
                                    (257, 512, 384)])
 def test_gemm_8phase(cuda, M, N, K):
@@ -344,6 +350,7 @@ def test_gemm_8phase(cuda, M, N, K):
         K_.gemm_set_variant(0)
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(4096, 3840, 1280, 32, 1280, 2048), (1000, 768, 640, 32, 256, 0),
                                                       (4100, 1024, 640, 96, 0, 4100), (520, 512, 192, 32, 512, 300),
                                                       (16384, 3840, 1280, 32, 1280, 8192)])
@@ -377,6 +384,7 @@ def test_gemm_8phase_lora_tail_paired_resid(cuda, M, N, K, K2, group, tail_rows)
         K_.gemm_set_variant(0)
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (1000, 640, 640, 32, 640, 0),
                                                       (4100, 1920, 640, 32, 640, 2048), (300, 320, 192, 0, 0, 0),
                                                       (8192, 1280, 5120, 32, 0, 4096), (257, 640, 64, 96, 320, 100)])
@@ -414,6 +422,7 @@ def test_gemm_8phase_256x160(cuda, M, N, K, K2, group, tail_rows):
         K_.gemm_set_variant(0)
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("M,N,K,K2,group,tail_rows", [(16384, 1280, 1280, 0, 0, 0), (16384, 1280, 1280, 32, 0, 8192),
                                                       (1000, 640, 640, 32, 320, 0), (4100, 1920, 640, 32, 640, 2048),
                                                       (300, 320, 192, 0, 0, 0), (8192, 1280, 5120, 64, 0, 4096),
@@ -458,6 +467,7 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
         K_.gemm_set_variant(0)
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [0, 31, 45])
 @pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100),
                                              (8192, 2560, 640, 0)])
@@ -498,6 +508,7 @@ def test_gemm_geglu_fwd_bwd_paths(cuda, variant, M, Fd, K, pre_rows):
         K_.gemm_set_variant(0)
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [0, 44])
 @pytest.mark.parametrize("B,C,H,W,Cout", [(2, 320, 64, 64, 320), (1, 640, 32, 32, 640), (3, 1280, 16, 16, 1280),
                                           (2, 64, 8, 32, 320), (1, 128, 32, 8, 640), (2, 192, 16, 16, 960)])
@@ -531,6 +542,7 @@ def test_conv_8phase_256x320(cuda, variant, B, C, H, W, Cout):
     assert _rel(_nchw(out.float()), ref) < 4e-3
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [0, 1, 3, 4, 6, 7, 8, 10, 11, 12, 14, 16, 17, 18, 19, 41])
 def test_conv_every_variant_large(cuda, variant):
     from pairwise_sample_optimization_amd import kernels as K_

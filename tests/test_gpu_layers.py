@@ -115,6 +115,7 @@ def test_attention_partial_tiles_poisoned_tail(cuda, B, H, Sq, Sk):
         assert torch.isfinite(got).all() and _rel(got, want) < 2e-2
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [2, 4])
 @pytest.mark.parametrize("B,H,Sq,Sk", [(2, 2, 256, 256), (2, 5, 300, 77), (1, 4, 130, 1000), (3, 20, 1024, 1024)])
 def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
@@ -145,6 +146,7 @@ def test_attention_fwd_tiles(cuda, variant, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [2, 4, 7, 9])  # 2 / 4: deferred-rescale forward, 32 / 64 rows per wave; 7 / 9: first-round loop
 @pytest.mark.parametrize("case", ["ramp", "spike"])
 def test_attention_fwd_rescale_paths(cuda, variant, case):
@@ -178,6 +180,7 @@ def test_attention_fwd_rescale_paths(cuda, variant, case):
     assert (o.float() - ref).abs().max().item() < 0.06
 
 
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [0, 32])  # 0: 2-phase 256x256 kernel; 32: the 8-phase kernel where K % 128 == 0
 @pytest.mark.parametrize("M,dim", [(8192, 1280), (300, 64), (1000, 640)])
 def test_gemm_geglu_fused(cuda, M, dim, variant):

@@ -6,6 +6,7 @@ workgroup 12.1 / 12.4 vs 11.9 ms; the contiguous element layout (PSO_ADAM8_LAYOU
 vs 11.88 / 11.96 ms on one box, same bits; byte-offset search 10.86, branch-free non-finite skip 10.50 ms.
 usage (GPU): python tools/adam8_bench.py [n_params]"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 import time
 

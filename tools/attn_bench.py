@@ -1,6 +1,7 @@
 """Micro-benchmark of the flash-attention kernels on the SDXL UNet shapes (8 images at 1024^2).
 usage: ATTN_VARIANTS=0,22,44 (fwd + 10*bwd) python tools/attn_bench.py   (GPU)"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

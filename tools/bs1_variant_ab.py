@@ -2,6 +2,7 @@
 C5 DreamBooth micro-step shapes, alternating arms; CONFIG=c3 / c2 runs the bench's c3 object / the C2 headline instead.
 usage (GPU): GEMM_VARIANTS=0,55 [CONFIG=c3] python tools/bs1_variant_ab.py [rounds]"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 import time
 

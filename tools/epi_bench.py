@@ -2,6 +2,7 @@
 (M=16384 / 8192, N=1280, K=1280): plain / +bias / +bias+resid / +LoRA tail / +tail limited to the policy rows.
 EPI_FLUSH=1 streams a 512 MB buffer between launches so every operand comes from HBM as in the train step."""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

@@ -3,6 +3,7 @@
 CU count when each CU's store stream is the limit, and grows with it when the chip's write bandwidth is.
 usage: python tools/epi_rate.py  (GPU)"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

@@ -2,6 +2,7 @@
 N % 160 shapes at 16 images (variant 37 = 2-phase, 38 = 8-phase; 'loop' = 8-phase with the epilogue skipped).
 usage: python tools/g160_bench.py  (GPU)"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

@@ -2,6 +2,7 @@
 and without its epilogue (main loop alone), against torch.matmul (hipBLASLt) on the same operands.
 usage: python tools/g256_bench.py  (GPU; GEMM_VARIANTS=0,39 to add dispatch variants)"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

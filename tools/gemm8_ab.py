@@ -2,6 +2,7 @@
 UNet's N % 256 shapes, interleaved rounds, with a max-error check of each mode against an fp32 product.  (GPU)"""
 import ctypes
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

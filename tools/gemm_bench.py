@@ -1,6 +1,7 @@
 """Micro-benchmark of the MFMA GEMM / implicit-GEMM conv kernel on the SDXL UNet's dominant shapes (1024^2, B=4)."""
 import sys
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

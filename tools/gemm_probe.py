@@ -3,6 +3,7 @@ with and without its epilogue stores, and the 8-phase kernel at K, 2K, 4K (per-K
 plus hipBLASLt (torch.mm) for reference.  Random bf16 operands."""
 import ctypes
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

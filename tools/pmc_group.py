@@ -2,6 +2,7 @@
 REPS launches of each shape, in a fixed order, so the counter rows map back to (group, shape) by dispatch index.
 Prints the launch plan; tools/parse_pmc_group.py joins it with the counter CSV."""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 import json
 import torch

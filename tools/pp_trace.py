@@ -5,6 +5,7 @@ usage (GPU): PP_VARIANTS=1080,1090 python tools/pp_trace.py   (1000s digit: trac
 9x with raised A-segment priority -- see pso_attention_set_variant)"""
 import ctypes
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

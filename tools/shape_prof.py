@@ -1,6 +1,7 @@
 """Per-shape breakdown of the GEMM family inside one C2 train step (HIP events per launch, grouped by shape).
 usage: python tools/shape_prof.py [--top 40]  (GPU)"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 from collections import defaultdict
 

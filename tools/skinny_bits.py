@@ -3,6 +3,7 @@ step runs, so two processes under different PSO_SKINNY_VARIANT values can be com
 usage (GPU): PSO_SKINNY_VARIANT=4 python tools/skinny_bits.py; python tools/skinny_bits.py   (compare the digests)"""
 import hashlib
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

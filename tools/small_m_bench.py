@@ -3,6 +3,7 @@ the backward runs on the 2 policy images): every variant of pso_gemm_set_variant
 with the LoRA K-tail where the step has one, next to hipBLASLt (torch.mm) on the same operands.
 usage (GPU): GEMM_VARIANTS=0,3,6,12,20,21,22 python tools/small_m_bench.py"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

@@ -1,5 +1,6 @@
 """Split-count sweep of the TN GEMM (LoRA weight gradients) and timing of the skinny-N GEMM on UNet shapes."""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch

@@ -2,6 +2,7 @@
 automatic dispatch under each GEMM variant (56 = the 256 x 256 TN tiles off), and the rel-L2 distance to torch fp32.
 usage (GPU): python tools/tn_full_bench.py [variant ...]"""
 import os
+os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
 
 import torch
