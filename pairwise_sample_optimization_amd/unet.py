@@ -603,7 +603,13 @@ class BasicTransformerBlock(nn.Module):
         o1 = a1m.to_out[0]
         if lo:
             u_o1 = K.gemm(pol(a1), L.A_o1)
-            h1 = _gemm_fwd(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1, tail_rows=tr)
+            if ok8(C, C, "out"):  # (diagnostic kind, not in the default FP8_KINDS: DESIGN §7 #8 table)
+                h1 = K.gemm_fp8(K.quant_rows_fp8(a1), f8((id(self), "o1"), o1.weight), a2=K.quant_rows_fp8(u_o1),
+                                w2=f8((id(self), "sB_o1"), L.sB_o1, ver), bias=o1.bias, resid=x, tail_rows=tr)
+            else:
+                h1 = _gemm_fwd(a1, o1.weight, bias=o1.bias, resid=x, a2=u_o1, w2=L.sB_o1, tail_rows=tr)
+        elif ok8(C, C, "out"):
+            h1 = K.gemm_fp8(K.quant_rows_fp8(a1), f8((id(self), "o1"), o1.weight), bias=o1.bias, resid=x)
         else:
             h1 = K.gemm(a1, o1.weight, bias=o1.bias, resid=x)
         # --- cross attention over the 77 text tokens ---
@@ -634,7 +640,13 @@ class BasicTransformerBlock(nn.Module):
         o2 = a2m.to_out[0]
         if lo:
             u_o2 = K.gemm(pol(a2), L.A_o2)
-            h2 = _gemm_fwd(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2, tail_rows=tr)
+            if ok8(C, C, "out"):
+                h2 = K.gemm_fp8(K.quant_rows_fp8(a2), f8((id(self), "o2"), o2.weight), a2=K.quant_rows_fp8(u_o2),
+                                w2=f8((id(self), "sB_o2"), L.sB_o2, ver), bias=o2.bias, resid=h1, tail_rows=tr)
+            else:
+                h2 = _gemm_fwd(a2, o2.weight, bias=o2.bias, resid=h1, a2=u_o2, w2=L.sB_o2, tail_rows=tr)
+        elif ok8(C, C, "out"):
+            h2 = K.gemm_fp8(K.quant_rows_fp8(a2), f8((id(self), "o2"), o2.weight), bias=o2.bias, resid=h1)
         else:
             h2 = K.gemm(a2, o2.weight, bias=o2.bias, resid=h1)
         # --- GEGLU feed-forward ---
@@ -646,7 +658,10 @@ class BasicTransformerBlock(nn.Module):
                             pre_rows=Mp)
         else:
             gg = K.gemm_geglu(n3, ff.w_int, ff.b_int, out_pre=f, pre_rows=Mp)  # f: interleaved pre-activation (bwd)
-        h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
+        if ok8(C, ff.out.weight.shape[1], "ffout"):  # ff.net.2 (diagnostic kind: DESIGN §7 #8 table)
+            h3 = K.gemm_fp8(K.quant_rows_fp8(gg), f8((id(self), "ffout"), ff.out.weight), bias=ff.out.bias, resid=h2)
+        else:
+            h3 = K.gemm(gg, ff.out.weight, bias=ff.out.bias, resid=h2)
         if rt.save:  # the backward runs on the policy images only
             sv = dict(x=pol(x), st1=pol(st1), n1=pol(n1), qkv=pol(qkv), a1=pol(a1), lse1=pol(lse1), h1=pol(h1),
                       st2=pol(st2), n2=pol(n2), q2=pol(q2), kv3=pol(kv3), a2=pol(a2), lse2=pol(lse2), h2=pol(h2),

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.gpu
 @pytest.mark.timeout(1500)
-def test_knob_forms_in_tools_build(cuda):
+def test_knob_forms_in_tools_build(cuda, capsys):
     lib = os.path.join(ROOT, "pairwise_sample_optimization_amd", "libpso_amd_knobs.so")
     assert os.path.exists(lib), "libpso_amd_knobs.so not built (make -C pairwise_sample_optimization_amd/csrc)"
     env = dict(os.environ, PSO_LIB="knobs")
@@ -28,6 +28,11 @@ def test_knob_forms_in_tools_build(cuda):
            os.path.join(ROOT, "tests", "test_gpu_determinism.py")]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=1400)
     tail = (r.stdout[-4000:] + r.stderr[-2000:])
-    print(tail)
+    with capsys.disabled():  # the child's summary line belongs in the suite log
+        print("\n[tools-build child] " + (r.stdout.strip().splitlines() or ["(no output)"])[-1], flush=True)
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out_dir):
+        with open(os.path.join(out_dir, "knobs_child.log"), "w") as f:
+            f.write(r.stdout + r.stderr)
     assert r.returncode == 0, tail
     assert " passed" in r.stdout and " failed" not in r.stdout
