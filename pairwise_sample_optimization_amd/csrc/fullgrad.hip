@@ -221,16 +221,58 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, const b
   cs2_store<1>(acc, part + (size_t)blockIdx.y * N, nullptr, blockIdx.x * 512, N, red);
 }
 
-// out[g][n] += sum_j part[g*nbg + j][n], j in order
-__global__ void colsum_reduce_kernel(int G, int nbg, int N, const float* __restrict__ part, float* __restrict__ out,
-                                     long ldo) {
+// Ordered two-level reduction of row-block partials (colsum: part[g][R][N]; LN dparam: part[1][R][2C]):
+//   level 1: split s of S adds rows [s*ch, (s+1)*ch) of its group in row order -> p2[g][s][N]  (ch rows in flight
+//            8 at a time: a single pass over R = 1,536 partials per column was a 1,536-long dependent load chain)
+//   level 2: out[g][n] += sum over s of p2[g][s][n], s in order
+// The grouping (R, S, ch) is a function of the shape only, so the sums are bit-reproducible.
+__global__ __launch_bounds__(256) void ordered_reduce_l1_kernel(int R, int N, int S, int ch,
+                                                                const float* __restrict__ part,
+                                                                float* __restrict__ p2) {
+  const int n = blockIdx.x * 256 + threadIdx.x, sp = blockIdx.y, g = blockIdx.z;
+  if (n >= N) return;
+  const int j0 = sp * ch, j1 = min(R, j0 + ch);
+  const float* p = part + ((size_t)g * R) * N + n;
+  float acc = 0.f;
+  for (int j = j0; j < j1; j += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = j + u < j1 ? p[(size_t)(j + u) * N] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];  // row order (the trailing zeros add exactly)
+  }
+  p2[((size_t)g * S + sp) * N + n] = acc;
+}
+
+// level 2.  LN dparam (split2 = C): columns [0, C) -> dgamma, [C, 2C) -> dbeta; colsum (split2 = 0): out[g*ldo + n]
+__global__ void ordered_reduce_l2_kernel(int G, int N, int S, const float* __restrict__ p2, float* __restrict__ out,
+                                         long ldo, float* __restrict__ out2, int split2) {
   const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (i >= (long)G * N) return;
   const int g = (int)(i / N), n = (int)(i - (long)g * N);
-  const float* p = part + (size_t)g * nbg * N + n;
-  float s = 0.f;
-  for (int j = 0; j < nbg; ++j) s += p[(size_t)j * N];
-  out[(long)g * ldo + n] += s;
+  float acc = 0.f;
+  for (int sp = 0; sp < S; ++sp) acc += p2[((size_t)g * S + sp) * N + n];
+  if (split2 > 0) {
+    if (n < split2) out[n] += acc;
+    else out2[n - split2] += acc;
+  } else {
+    out[(long)g * ldo + n] += acc;
+  }
+}
+
+// split count of the level-1 pass: ~32 partial rows per split, at most 64 splits; R <= 48 partial rows take level 2
+// alone (S = R, ch = 1: the level-1 pass would copy them)
+static void ordered_reduce_plan(int R, int& S, int& ch) {
+  if (R <= 48) {
+    S = R;
+    ch = 1;
+    return;
+  }
+  S = (R + 31) / 32;
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
+  ch = (R + S - 1) / S;
+  S = (R + ch - 1) / ch;
 }
 
 __global__ __launch_bounds__(256) void ln_dparam_part_kernel(int M, int C, const bf16_t* __restrict__ x, long ldx,
@@ -257,17 +299,6 @@ __global__ __launch_bounds__(256) void ln_dparam_part_kernel(int M, int C, const
   }
   float* p = part + (size_t)blockIdx.y * 2 * C;
   cs2_store<2>(acc, p, p + C, blockIdx.x * 512, C, red);
-}
-
-// dgamma[c] += sum_j part[j][0][c], dbeta[c] += sum_j part[j][1][c], j in order
-__global__ void ln_dparam_reduce_kernel(int nb, int C, const float* __restrict__ part, float* __restrict__ dgamma,
-                                        float* __restrict__ dbeta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * C) return;
-  const int k = i / C, c = i - k * C;
-  float s = 0.f;
-  for (int j = 0; j < nb; ++j) s += part[((size_t)j * 2 + k) * C + c];
-  (k ? dbeta : dgamma)[c] += s;
 }
 
 // one thread per (output pixel, tap, 8-channel chunk)
@@ -352,7 +383,9 @@ static int colsum_nbg(long M, long rpg) { return (int)(((M < rpg ? M : rpg) + CS
 size_t pso_colsum_acc_ws_bytes(long M, int N, long rows_per_group) {
   if (M <= 0 || N <= 0 || rows_per_group <= 0) return 0;
   const long G = (M + rows_per_group - 1) / rows_per_group;
-  return (size_t)G * colsum_nbg(M, rows_per_group) * N * sizeof(float);
+  int S, ch;
+  ordered_reduce_plan(colsum_nbg(M, rows_per_group), S, ch);
+  return (size_t)G * (colsum_nbg(M, rows_per_group) + S) * N * sizeof(float);
 }
 
 int pso_colsum_acc_ws(long M, int N, const void* x, long ldx, long rows_per_group, float* out, long ldo, void* ws,
@@ -367,13 +400,21 @@ int pso_colsum_acc_ws(long M, int N, const void* x, long ldx, long rows_per_grou
   const hipStream_t st = (hipStream_t)stream;
   colsum_part_kernel<<<dim3((N + 511) / 512, (unsigned)(G * nbg)), 256, 0, st>>>(M, N, (const bf16_t*)x, ldx,
                                                                                 rows_per_group, nbg, vec, (float*)ws);
-  colsum_reduce_kernel<<<(unsigned)((G * N + 255) / 256), 256, 0, st>>>((int)G, nbg, N, (const float*)ws, out, ldo);
+  int S, ch;
+  ordered_reduce_plan(nbg, S, ch);
+  float* p2 = (float*)ws + (size_t)G * nbg * N;
+  if (ch == 1) p2 = (float*)ws;  // level 2 straight over the partials ([g][R][N] = [g][S][N])
+  else ordered_reduce_l1_kernel<<<dim3((N + 255) / 256, S, (unsigned)G), 256, 0, st>>>(nbg, N, S, ch, (const float*)ws, p2);
+  ordered_reduce_l2_kernel<<<(unsigned)((G * N + 255) / 256), 256, 0, st>>>((int)G, N, S, p2, out, ldo, nullptr, 0);
   return pso_check_launch("pso_colsum_acc_ws");
 }
 
 size_t pso_layer_norm_dparam_ws_bytes(int M, int C) {
   if (M <= 0 || C <= 0) return 0;
-  return (size_t)((M + CS2_ROWS - 1) / CS2_ROWS) * 2 * C * sizeof(float);
+  const int nb = (M + CS2_ROWS - 1) / CS2_ROWS;
+  int S, ch;
+  ordered_reduce_plan(nb, S, ch);
+  return (size_t)(nb + S) * 2 * C * sizeof(float);
 }
 
 int pso_layer_norm_dparam_ws(int M, int C, const void* x, long ldx, const void* dy, long lddy, const float* stats,
@@ -386,7 +427,12 @@ int pso_layer_norm_dparam_ws(int M, int C, const void* x, long ldx, const void* 
   const hipStream_t st = (hipStream_t)stream;
   ln_dparam_part_kernel<<<dim3((C + 511) / 512, nb), 256, 0, st>>>(M, C, (const bf16_t*)x, ldx, (const bf16_t*)dy,
                                                                   lddy, stats, vec, (float*)ws);
-  ln_dparam_reduce_kernel<<<(2 * C + 255) / 256, 256, 0, st>>>(nb, C, (const float*)ws, dgamma, dbeta);
+  int S, ch;
+  ordered_reduce_plan(nb, S, ch);
+  float* p2 = (float*)ws + (size_t)nb * 2 * C;
+  if (ch == 1) p2 = (float*)ws;
+  else ordered_reduce_l1_kernel<<<dim3((2 * C + 255) / 256, S, 1), 256, 0, st>>>(nb, 2 * C, S, ch, (const float*)ws, p2);
+  ordered_reduce_l2_kernel<<<(2 * C + 255) / 256, 256, 0, st>>>(1, 2 * C, S, p2, dgamma, 0, dbeta, C);
   return pso_check_launch("pso_layer_norm_dparam_ws");
 }
 

@@ -750,13 +750,31 @@ def axpby(a, x, b=0.0, z=None, out=None):
     return out
 
 
+_FULLGRAD_ATOMIC = os.environ.get("PSO_FULLGRAD_ATOMIC", "0") == "1"
+_STREAM_WS = {}  # (device index, stream handle) -> uint8 scratch of the ordered parameter-sum reductions
+
+
+def _stream_ws(nbytes, device):
+    """Scratch for a reduction issued on the current stream: one buffer per (device, stream), grown on demand.  Its
+    users are ordered by their stream, so reusing it needs no synchronisation (and no allocation per call)."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _STREAM_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = _STREAM_WS[key] = torch.empty(max(int(nbytes * 1.25), 1 << 16), device=device, dtype=torch.uint8)
+    return ws
+
+
 def colsum_acc(x, out, rows_per_group=None):
     """out [G, N] f32 += per-group column sums of x [M, N] bf16 (G = M / rows_per_group; bias / row-bias grads), in a
     fixed summation order (pso_colsum_acc_ws: per-row-block partials through a workspace, no float atomics)."""
     M, N = x.shape
     rpg = M if rows_per_group is None else rows_per_group
+    if _FULLGRAD_ATOMIC:  # A/B of the ordered form's cost (PSO_FULLGRAD_ATOMIC=1): f32 atomics, not reproducible
+        check(lib().pso_colsum_acc(M, N, ptr(x), _row_stride(x), rpg, ptr(out),
+                                   out.stride(0) if out.dim() > 1 else N, stream_ptr()), "pso_colsum_acc")
+        return out
     wsb = int(lib().pso_colsum_acc_ws_bytes(M, N, rpg))
-    ws = torch.empty(max(wsb, 16), device=x.device, dtype=torch.uint8)
+    ws = _stream_ws(wsb, x.device)
     check(lib().pso_colsum_acc_ws(M, N, ptr(x), _row_stride(x), rpg, ptr(out), out.stride(0) if out.dim() > 1 else N,
                                   ptr(ws), ws.numel(), stream_ptr()), "pso_colsum_acc_ws")
     return out
@@ -766,8 +784,12 @@ def layer_norm_dparam(x, dy, stats, dgamma, dbeta):
     """dgamma / dbeta [C] f32 += LayerNorm weight / bias grads (stats from layer_norm_fwd), in a fixed summation order
     (pso_layer_norm_dparam_ws)."""
     M, C = x.shape
+    if _FULLGRAD_ATOMIC:
+        check(lib().pso_layer_norm_dparam(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats),
+                                          ptr(dgamma), ptr(dbeta), stream_ptr()), "pso_layer_norm_dparam")
+        return
     wsb = int(lib().pso_layer_norm_dparam_ws_bytes(M, C))
-    ws = torch.empty(max(wsb, 16), device=x.device, dtype=torch.uint8)
+    ws = _stream_ws(wsb, x.device)
     check(lib().pso_layer_norm_dparam_ws(M, C, ptr(x), _row_stride(x), ptr(dy), _row_stride(dy), ptr(stats),
                                          ptr(dgamma), ptr(dbeta), ptr(ws), ws.numel(), stream_ptr()),
           "pso_layer_norm_dparam_ws")
