@@ -820,6 +820,8 @@ int pso_gemm8p320_conv_run(int B, int H, int W, int C, const void* x, const void
                            void* out, long ldo, int group_m, hipStream_t st);
 int pso_gemm8p320_geglu_bwd_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* aux,
                                 long ldaux, void* out, long ldo, int group_m, hipStream_t st);
+int pso_gemm8p320_geglu_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
+                            void* out, long ldo, void* out2, long ldo2, int pre_rows, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
 
 // Ordered reduction of the split-K partials + the plain epilogue (4 consecutive columns per thread, N % 4 == 0):
@@ -907,9 +909,9 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
-// the variants 37-56 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// the variants 37-57 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
 // 256 x 160 8-phase tiles off / forced; 56 = the 256 x 256 TN tiles off; ...); any other non-zero variant forces one tile shape
-static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 56) ? 0 : gv_raw; }
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 57) ? 0 : gv_raw; }
 // the workspace split-K forms (pso_gemm_ws / pso_conv2d_ws) under the benchmark knobs: off where a variant forces a
 // tile (38 / 39 / 44: the 8-phase 256 x 160 / 256 x 320 / conv tiles, the tests that pin them), where a raster group
 // is forced, and under variant 52 (the conv split off)
@@ -1839,6 +1841,16 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   // the 8-phase kernel with the LDS-staged epilogue (gemm8p.hip): 16384 x 10240 x 1280 1023 vs 801 TF/s,
   // 65536 x 5120 x 640 814 vs 640 (tools/gemm_bench.py, one box), inside the C2 step 1006 vs 922 / 801 vs 706
   // (tools/shape_prof.py); variant 31 keeps the 2-phase 256x256 kernel
+  // 256 x 320 tiles where they cost fewer tile-rounds than 256 x 256 (rounds x tile width: bs = 1's 4096 x 10240:
+  // 2 x 320 < 3 x 256; C3's 6144 x 10240: 3 x 320 < 4 x 256; C5's 2048 x 10240: 1 x 320 < 2 x 256; equal at C2's
+  // whole-round shapes, which keep 256 x 256); same bits either way.  Variant 57 keeps 256 x 256.
+  if (g_gemm_variant != 31 && g_gemm_variant != 57 && (K % 64) == 0 && (N % 320) == 0 && lda == ldw &&
+      fits30(M, lda) && fits30(N, ldw)) {
+    const long r256 = ((long)((M + 255) / 256) * (N / 256) + 255) / 256, r320 = ((long)((M + 255) / 256) * (N / 320) + 255) / 256;
+    if (r320 * 320 < r256 * 256)
+      return pso_gemm8p320_geglu_run(M, N, K, a, lda, w, ldw, bias, out, ldo, out_pre, ld_pre, g.tail_m, g.group_m,
+                                     (hipStream_t)stream);
+  }
   if (g_gemm_variant != 31 && (K % 64) == 0 && fits30(M, lda) && fits30(N, ldw))
     return pso_gemm8p_run(1, M, N, K, a, lda, w, ldw, nullptr, 0, 0, nullptr, 0, 0, 0, 1.f, bias, nullptr, 0, out, ldo,
                           out_pre, ld_pre, g.tail_m, nullptr, 0, g.group_m, (hipStream_t)stream);

@@ -112,8 +112,8 @@ __device__ __forceinline__ void mfma8s(i32x8 w, i32x8 x, f32x4& c, int sb, int s
 template <int EPI, bool STAG, bool SPRIO, bool FP8 = false, int BN = 256, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
   static_assert(BN == 256 || ((BN == 160 || BN == 320) && !FP8 && (EPI == EPI8_NONE ||
-                                                                     (BN == 320 && EPI == EPI8_GEGLU_BWD && !CONV))),
-                "256 x 160 / 256 x 320 tiles: bf16, plain epilogue (320: also the GEGLU backward)");
+                                                                     (BN == 320 && EPI != EPI8_NONE && !CONV))),
+                "256 x 160 / 256 x 320 tiles: bf16, plain epilogue (320: also the GEGLU forward and backward)");
   static_assert(!CONV || BN == 320, "implicit-GEMM conv: 256 x 320 tiles only");
   constexpr int ES = FP8 ? 1 : 2;         // bytes per operand element
   constexpr int KT = FP8 ? 128 : 64;      // K elements per K-tile (always 128 B per row)
@@ -590,6 +590,41 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(Gemm8Args g) {
       }
     };
     auto store_half = [&](int ha) {
+      if constexpr (EPI == EPI8_GEGLU) {
+        // the staged half IS the interleaved pre-activation ([h 32 | gate 32] per 64 columns, acc + bias rounded
+        // once, as in the 256 x 256 form): its policy rows (< pre_rows) to out2, then out = h * gelu(gate) from it --
+        // the 256 x 256 form's arithmetic on the same bf16 values, so the same bits
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g.out2) {
+#pragma unroll 2
+          for (int p = 0; p < 10; ++p) {  // 128 rows x 40 chunks = 10 passes of 512
+            const int idx = p * 512 + tid;
+            const int R = idx / 40, c = idx - R * 40, m = m0 + ha * 128 + R;
+            if (m < g.pre_rows && m < g.M)
+              *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out2) + (long)m * g.ldo2 + n0 + c * 8) =
+                  *reinterpret_cast<const uint4*>(tl + R * TP + c * 8);
+          }
+        }
+        // output chunk q (20 per row: 160 output columns) = h chunk (q / 4) * 8 + (q % 4), gate chunk + 4
+#pragma unroll 1
+        for (int p = 0; p < 5; ++p) {  // 128 rows x 20 chunks = 5 passes of 512
+          const int idx = p * 512 + tid;
+          const int R = idx / 20, q = idx - R * 20, m = m0 + ha * 128 + R;
+          if (m >= g.M) continue;
+          const int ch = (q >> 2) * 8 + (q & 3);
+          const uint4 hv = *reinterpret_cast<const uint4*>(tl + R * TP + ch * 8);
+          const uint4 gv = *reinterpret_cast<const uint4*>(tl + R * TP + (ch + 4) * 8);
+          const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = pack2bf(bf2f(hw[e] & 0xffff) * gelu_erf(bf2f(gw[e] & 0xffff)),
+                           bf2f(hw[e] >> 16) * gelu_erf(bf2f(gw[e] >> 16)));
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + (long)m * g.ldo + n0 / 2 + q * 8) =
+              make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        return;
+      }
       if constexpr (EPI == EPI8_GEGLU_BWD) {
         // the staged half = dout (bf16, as the unfused path stores it); chunk c of row R = dout columns n .. n+7 ->
         // interleaved input-gradient positions ph .. ph+7 (h) and ph+32 .. (gate), ph = (n / 32) * 64 + n % 32, from
@@ -975,6 +1010,19 @@ int pso_gemm8p320_run(int M, int N, int K, const void* a, long lda, const void* 
   g.alpha = alpha; g.bias = (const bf16_t*)bias; g.resid = (const bf16_t*)resid; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.group_m = group_m; g.skip_epi = g_skip_epi8;
   return launch8<EPI8_NONE, true, false, false, 320>(g, st);
+}
+
+// GEGLU forward on 256 x 320 tiles (N % 320 == 0, lda == ldw; preconditions checked in gemm.hip): the interleaved
+// pre-activation a . w^T + bias (rows < pre_rows to out2) and out = h * gelu(gate), bit-identical to the 256 x 256 form
+int pso_gemm8p320_geglu_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
+                            void* out, long ldo, void* out2, long ldo2, int pre_rows, int group_m, hipStream_t st) {
+  Gemm8Args g{};
+  g.a = (const bf16_t*)a; g.lda = lda; g.w = (const bf16_t*)w; g.ldw = ldw;
+  g.M = M; g.N = N; g.K = K; g.tail_m = M;
+  g.alpha = 1.f; g.bias = (const bf16_t*)bias;
+  g.out = out; g.ldo = ldo; g.out2 = out2; g.ldo2 = ldo2; g.pre_rows = pre_rows;
+  g.group_m = group_m; g.skip_epi = g_skip_epi8;
+  return launch8<EPI8_GEGLU, true, false, false, 320>(g, st);
 }
 
 // GEGLU backward on 256 x 320 tiles (N % 320 == 0, lda == ldw; preconditions checked in gemm.hip): dout = a . w^T,

@@ -468,6 +468,45 @@ def test_gemm_8phase_256x320(cuda, M, N, K, K2, group, tail_rows):
 
 
 @pytest.mark.knobs
+@pytest.mark.parametrize("variant", [0, 57])
+@pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (6144, 5120, 1280, 0), (2048, 5120, 1280, 1024),
+                                             (24576, 2560, 640, 12288), (1900, 5120, 640, 950)])
+def test_gemm_geglu_320_tiles(cuda, variant, M, Fd, K, pre_rows):
+    """The GEGLU projection on 256 x 320 tiles where they cost fewer tile-rounds than 256 x 256 (bs = 1's 4096 x 10240,
+    C3's 6144 x 10240 and 24576 x 5120, C5's 2048 x 10240, a ragged M): against torch fp32, and -- in the tools build --
+    bit for bit against the 256 x 256 form (variant 57): the same accumulation order and the same epilogue arithmetic on
+    the same bf16 pre-activations."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    g = torch.Generator(device="cuda").manual_seed(M + Fd + 1)
+    x = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    wp = (torch.randn(2 * Fd, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    bp = torch.randn(2 * Fd, device=cuda, generator=g).bfloat16()
+    idx = K_.geglu_interleave_index(Fd, cuda)
+    wi, bi = wp[idx].contiguous(), bp[idx].contiguous()
+    pr = pre_rows or M
+
+    def run():
+        pre = torch.full((pr, 2 * Fd), float("nan"), device=cuda, dtype=torch.bfloat16)
+        out = K_.gemm_geglu(x, wi, bi, out_pre=pre, pre_rows=pre_rows)
+        return out, pre, K_.lib().pso_last_kernel().decode()
+
+    out, pre, kn = run()
+    assert kn == "gemm8p_kernel<1, true, false, false, 320, false>", kn
+    hg = (x.float() @ wp.float().t() + bp.float()).bfloat16().float()
+    h, gt = hg[:, :Fd], hg[:, Fd:]
+    assert _rel(out, h * F.gelu(gt)) < 4e-3
+    assert _rel(pre, hg[:pr, idx]) < 4e-3 and not torch.isnan(pre).any()
+    if variant:
+        K_.gemm_set_variant(variant)
+        try:
+            out2, pre2, kn2 = run()
+        finally:
+            K_.gemm_set_variant(0)
+        assert kn2 == "gemm8p_kernel<1, true, false, false, 256, false>", kn2
+        assert torch.equal(out, out2) and torch.equal(pre, pre2)
+
+
+@pytest.mark.knobs
 @pytest.mark.parametrize("variant", [0, 31, 45])
 @pytest.mark.parametrize("M,Fd,K,pre_rows", [(4096, 5120, 1280, 2048), (1000, 2560, 640, 0), (300, 1280, 320, 100),
                                              (8192, 2560, 640, 0)])
