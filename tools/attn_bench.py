@@ -1,5 +1,6 @@
 """Micro-benchmark of the flash-attention kernels on the SDXL UNet shapes (8 images at 1024^2).
 usage: ATTN_VARIANTS=0,22,44 (fwd + 10*bwd) python tools/attn_bench.py   (GPU)"""
+import hashlib
 import os
 os.environ.setdefault("PSO_LIB", "knobs")  # benchmark knobs: the tools build (include/pso_amd_knobs.h)
 import sys
@@ -51,8 +52,10 @@ def main():
                                                             for x, y in zip(grads, ref[name])))
             else:
                 ref[name] = [x.clone() for x in grads]
+            # digest of the outputs: compares builds of the same sources (same-box library A/B via PSO_LIB_PATH)
+            dig = hashlib.sha1(b"".join(x.view(torch.int16).cpu().numpy().tobytes() for x in (o, *grads))).hexdigest()
             print(f"{name:10s} B{B} H{H} {Sq}x{Sk}: fwd {ms:7.3f} ms {fl / ms / 1e9:7.1f} TF/s | "
-                  f"bwd {msb:7.3f} ms {2.5 * fl / msb / 1e9:7.1f} TF/s (2.5x fwd flop){same}", flush=True)
+                  f"bwd {msb:7.3f} ms {2.5 * fl / msb / 1e9:7.1f} TF/s (2.5x fwd flop){same} sha1 {dig[:12]}", flush=True)
     K.lib().pso_attention_set_variant(0)
 
 
