@@ -14,7 +14,13 @@
 // Backward also emits per-channel dgamma/dbeta partial sums (full-UNet gradients, config 3) when asked.
 #include "common.h"
 
-#define GN_ROWS 64  // pixels per partial block
+#define GN_ROWS 64  // pixels per partial / apply block
+// Pixels per block of the forward passes above 256 blocks of GN_ROWS per image (HW > 16384: only the VAE's 256^2 -
+// 1024^2 levels; every UNet GroupNorm has HW <= 128^2 and keeps GN_ROWS and its bits): 8x fewer partial rows for the
+// finalize pass's serial combine, and 8x longer blocks (16 pixel rows per thread at C = 128 instead of 2); VAE decode
+// 127.7 -> 113.0 ms per 8 images at 512 (256: 114.1-114.8, 1024: 113.3-113.7; profiles/r06_vae_groupnorm_ab.log)
+#define GN_ROWS_BIG 512
+static int gn_rows_fwd(int HW) { return (HW + GN_ROWS - 1) / GN_ROWS > 256 ? GN_ROWS_BIG : GN_ROWS; }
 
 __device__ __forceinline__ void unpack8(uint4 v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -36,7 +42,7 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __ex
 // ws layout: [B][chunks][G][2] (+ per-channel [B][chunks][C][2] after it when DPARAM)
 // ---------------------------------------------------------------------------------------------------------------
 template <bool BWD, bool SILU>
-__global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+__global__ void gn_partial_kernel(int HW, int rows, int C, int G, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                   const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
                                   const bf16_t* __restrict__ beta, float* __restrict__ ws, float* __restrict__ ws_ch) {
   extern __shared__ float red[];  // [RS][C][2]
@@ -44,7 +50,7 @@ __global__ void gn_partial_kernel(int HW, int C, int G, const bf16_t* __restrict
   const int RS = blockDim.x / TPR;
   const int slot = threadIdx.x / TPR, cc = threadIdx.x - slot * TPR;
   const int b = blockIdx.y, chunk = blockIdx.x, nchunks = gridDim.x;
-  const int r0 = chunk * GN_ROWS, r1 = min(HW, r0 + GN_ROWS);
+  const int r0 = chunk * rows, r1 = min(HW, r0 + rows);
   const int Cg = C / G;
   float s1[8], s2[8];
 #pragma unroll
@@ -220,7 +226,7 @@ __global__ void gn_dparam_final_kernel(int C, int S, const double* __restrict__ 
 // mean / rstd / gamma / beta of its 8 channels into per-channel (scale, shift) once and streams its pixel rows with
 // one FMA (+ SiLU) per element -- no per-element divisions or scalar parameter loads.
 template <bool SILU>
-__global__ void gn_apply_fwd_kernel(int HW, int C, int G, const bf16_t* __restrict__ x, const float* __restrict__ stats,
+__global__ void gn_apply_fwd_kernel(int HW, int rows, int C, int G, const bf16_t* __restrict__ x, const float* __restrict__ stats,
                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
                                     bf16_t* __restrict__ y) {
   const int TPR = C / 8;
@@ -228,7 +234,7 @@ __global__ void gn_apply_fwd_kernel(int HW, int C, int G, const bf16_t* __restri
   const int slot = threadIdx.x / TPR, cc = threadIdx.x - slot * TPR;
   if (slot >= RS) return;
   const int b = blockIdx.y;
-  const int r0 = blockIdx.x * GN_ROWS, r1 = min(HW, r0 + GN_ROWS);
+  const int r0 = blockIdx.x * rows, r1 = min(HW, r0 + rows);
   const int Cg = C / G;
   float sc[8], sh[8];
 #pragma unroll
@@ -424,19 +430,20 @@ int pso_group_norm_fwd(int B, int HW, int C, int G, float eps, const void* x, co
   PSO_ARG_CHECK(x && y && stats && ws, "pso_group_norm_fwd: null pointer");
   PSO_ARG_CHECK(ws_bytes >= pso_group_norm_ws_bytes(B, HW, C), "pso_group_norm_fwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  const int nchunks = cdiv(HW, GN_ROWS);
+  const int rows = gn_rows_fwd(HW);
+  const int nchunks = cdiv(HW, rows);
   const int threads = gn_block(C);
   const size_t shm = (size_t)(threads / (C / 8)) * C * 2 * sizeof(float);
-  gn_partial_kernel<false, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, (const bf16_t*)x, nullptr,
+  gn_partial_kernel<false, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, rows, C, G, (const bf16_t*)x, nullptr,
                                                                           nullptr, nullptr, nullptr, (float*)ws,
                                                                           nullptr);
   gn_finalize_kernel<false><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, eps, (const float*)ws, stats);
   if (silu)
-    gn_apply_fwd_kernel<true><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, (const bf16_t*)x, stats,
+    gn_apply_fwd_kernel<true><<<dim3(nchunks, B), threads, 0, st>>>(HW, rows, C, G, (const bf16_t*)x, stats,
                                                                     (const bf16_t*)gamma, (const bf16_t*)beta,
                                                                     (bf16_t*)y);
   else
-    gn_apply_fwd_kernel<false><<<dim3(nchunks, B), threads, 0, st>>>(HW, C, G, (const bf16_t*)x, stats,
+    gn_apply_fwd_kernel<false><<<dim3(nchunks, B), threads, 0, st>>>(HW, rows, C, G, (const bf16_t*)x, stats,
                                                                      (const bf16_t*)gamma, (const bf16_t*)beta,
                                                                      (bf16_t*)y);
   return pso_check_launch("pso_group_norm_fwd");
@@ -460,11 +467,11 @@ int pso_group_norm_bwd(int B, int HW, int C, int G, const void* x, const void* d
   const bf16_t *xp = (const bf16_t*)x, *dyp = (const bf16_t*)dy, *gp = (const bf16_t*)gamma,
                *bp = (const bf16_t*)beta;
   if (silu)
-    gn_partial_kernel<true, true><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part,
-                                                                          part_ch);
+    gn_partial_kernel<true, true><<<dim3(nchunks, B), threads, shm, st>>>(HW, GN_ROWS, C, G, xp, dyp, stats, gp, bp,
+                                                                          part, part_ch);
   else
-    gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, C, G, xp, dyp, stats, gp, bp, part,
-                                                                           part_ch);
+    gn_partial_kernel<true, false><<<dim3(nchunks, B), threads, shm, st>>>(HW, GN_ROWS, C, G, xp, dyp, stats, gp, bp,
+                                                                           part, part_ch);
   gn_finalize_kernel<true><<<cdiv(B * G, 4), 256, 0, st>>>(B, HW, C, G, nchunks, 0.f, part, coef);
   if (dgamma || dbeta) {
     // the group partials (part) are consumed by gn_finalize above: their space takes the split sums (S <= B*chunks/2
