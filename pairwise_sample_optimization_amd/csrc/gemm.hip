@@ -909,9 +909,9 @@ int pso_gemm_group_knob() { return g_gemm_group; }  // gemm8p.hip: a forced grou
 // 239.2 / 238.9 / 240.5 / 241.9 ms
 #define PSO_GEMM_GROUP_M 4
 
-// the variants 37-57 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
+// the variants 37-58 keep the automatic dispatch and flip one of its rules (41 = per-lane epilogue; 37 / 38 = the
 // 256 x 160 8-phase tiles off / forced; 56 = the 256 x 256 TN tiles off; ...); any other non-zero variant forces one tile shape
-static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 57) ? 0 : gv_raw; }
+static int gemm_auto_variant(int gv_raw) { return (gv_raw >= 37 && gv_raw <= 58) ? 0 : gv_raw; }
 // the workspace split-K forms (pso_gemm_ws / pso_conv2d_ws) under the benchmark knobs: off where a variant forces a
 // tile (38 / 39 / 44: the 8-phase 256 x 160 / 256 x 320 / conv tiles, the tests that pin them), where a raster group
 // is forced, and under variant 52 (the conv split off)
@@ -1847,7 +1847,8 @@ int pso_gemm_geglu(int M, int N, const void* a, long lda, int K, const void* w, 
   if (g_gemm_variant != 31 && g_gemm_variant != 57 && (K % 64) == 0 && (N % 320) == 0 && lda == ldw &&
       fits30(M, lda) && fits30(N, ldw)) {
     const long r256 = ((long)((M + 255) / 256) * (N / 256) + 255) / 256, r320 = ((long)((M + 255) / 256) * (N / 320) + 255) / 256;
-    if (r320 * 320 < r256 * 256)
+    // variant 58 (knob): 256 x 320 at equal rounds too (C2's shapes)
+    if (r320 * 320 < r256 * 256 || (g_gemm_variant == 58 && r320 * 320 == r256 * 256))
       return pso_gemm8p320_geglu_run(M, N, K, a, lda, w, ldw, bias, out, ldo, out_pre, ld_pre, g.tail_m, g.group_m,
                                      (hipStream_t)stream);
   }
