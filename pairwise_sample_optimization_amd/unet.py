@@ -244,6 +244,19 @@ _FULL_SIDE = os.environ.get("PSO_FULL_SIDE_STREAM", "1") == "1"
 # enable_fp8_forward
 FP8_KINDS = {"q2", "ff", "tail"}
 FP8_MIN_TILES = int(os.environ.get("PSO_FP8_MIN_TILES", "192"))  # see BasicTransformerBlock.fwd (0: no occupancy rule)
+# The e4m3 GEGLU form has 256 x 256 tiles only, while the bf16 one takes 256 x 320 tiles where they need fewer
+# tile-rounds (gemm.hip pso_gemm_geglu: rounds x tile width).  A round of e4m3 tiles costs ~1/1.3 of a bf16 one on
+# these shapes (the 2x MFMA rate less the row quantisation and the longer prologue: C5's GEGLU 5.7 -> 4.2 ms at equal
+# tiles), so the ff kind stays on e4m3 only while its rounds x 256 undercut 1.3 x the bf16 form's rounds x width.
+FP8_ROUND_GAIN = 1.3
+
+
+def fp8_geglu_pays(M, n_out):
+    """True when the e4m3 GEGLU projection (256 x 256 tiles) is expected to beat the bf16 one's tile choice."""
+    mt = (M + 255) // 256
+    w8 = (mt * (n_out // 256) + 255) // 256 * 256
+    w16 = w8 if n_out % 320 else min(w8, (mt * (n_out // 320) + 255) // 256 * 320)
+    return w8 < FP8_ROUND_GAIN * w16
 _GEGLU_TN = os.environ.get("PSO_GEGLU_TN", "1") == "1"
 # diagnostics (tools/c2_window_diag.py): the forward's LoRA-augmented projections rounded as torch/peft round them --
 # bf16(base + bias), bf16(LoRA term), bf16 add, then bf16 residual add -- instead of one rounding of the fused sum
@@ -653,7 +666,7 @@ class BasicTransformerBlock(nn.Module):
         n3, st3 = K.layer_norm_fwd(h2, self.norm3.weight, self.norm3.bias, 1e-5)
         ff = self.ff
         f = torch.empty((Mp, ff.w_int.shape[0]), device=x.device, dtype=BF16) if rt.save else None
-        if ok8(ff.w_int.shape[0], C, "ff"):
+        if ok8(ff.w_int.shape[0], C, "ff") and fp8_geglu_pays(M, ff.w_int.shape[0]):
             gg = K.gemm_fp8(K.quant_rows_fp8(n3), f8((id(self), "ff"), ff.w_int), bias=ff.b_int, geglu=True, out_pre=f,
                             pre_rows=Mp)
         else:

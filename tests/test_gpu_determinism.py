@@ -205,6 +205,7 @@ def test_graph_epoch_equals_eager_epoch_fp8(cuda, monkeypatch):
     # lift the occupancy rule (192 tiles) so the sdxl32 products really run on e4m3 and the replay reads the fp8
     # sB cache this test guards
     monkeypatch.setattr(U, "FP8_MIN_TILES", 0)
+    monkeypatch.setattr(U, "FP8_ROUND_GAIN", 1e9)  # and the GEGLU round-cost rule: every fp8 kind runs e4m3
     cfg = UNetConfig.sdxl(32)
     P, gas = 1, 2
 

@@ -118,6 +118,7 @@ def test_unet_fp8_forward_eps_and_lora_grads_vs_fp32(cuda, which, monkeypatch):
     # the occupancy rule (FP8_MIN_TILES = 192 tiles of 256 x 256) keeps every product of these small UNets on bf16:
     # lift it so the e4m3 kernels run here
     monkeypatch.setattr(U, "FP8_MIN_TILES", 0)
+    monkeypatch.setattr(U, "FP8_ROUND_GAIN", 1e9)  # and the GEGLU round-cost rule: every fp8 kind runs e4m3
     cfg = UNetConfig.sdxl(32 if which == "sdxl32" else 64)
     unet, sample, t, enc, text, tid = _setup(cuda, cfg, r=16)  # rank 16 (the DreamBooth recipe): fp8 LoRA tails
     add = {"text_embeds": text, "time_ids": tid}
