@@ -823,6 +823,8 @@ int pso_gemm8p320_geglu_bwd_run(int M, int N, int K, const void* a, long lda, co
 int pso_gemm8p320_geglu_run(int M, int N, int K, const void* a, long lda, const void* w, long ldw, const void* bias,
                             void* out, long ldo, void* out2, long ldo2, int pre_rows, int group_m, hipStream_t st);
 static bool fits30(long rows, long ld) { return rows * ld < (1L << 30); }
+int pso_conv3x3_smallc_run(int B, int H, int W, int Cin, int Cout, const void* x, const void* w, const void* bias,
+                           void* out, hipStream_t st);  // conv_small.hip
 
 // Ordered reduction of the split-K partials + the plain epilogue (4 consecutive columns per thread, N % 4 == 0):
 //   y = alpha * sum_s ws[s][m][n] + bias[n] + rowbias[m / rows_per_group][n]
@@ -1756,6 +1758,12 @@ int pso_conv2d(int mode, int B, const void* src1, int C1, const void* src2, int 
   PSO_ARG_CHECK(mode != PSO_CONV_UP2 || (Ho == 2 * H && Wo == 2 * W && stride == 1), "pso_conv2d: UP2 geometry");
   PSO_ARG_CHECK(!a2 || ((K2 % 8) == 0 && b2 && al16(a2) && al16(b2)), "pso_conv2d: bad second operand");
   PSO_ARG_CHECK(!accumulate || out_dtype == PSO_F32, "pso_conv2d: accumulate needs f32 output");
+  // Cout <= 3 (the VAE decoder's conv_out to RGB): a direct convolution instead of an N = 3 GEMM padded to 64-column
+  // MFMA tiles (conv_small.hip; 1024^2: 1.34 ms -> see DESIGN §4 / profiles/r06_vae_conv_out_ab.log)
+  if (mode == PSO_CONV_NORMAL && ks == 3 && stride == 1 && pad == 1 && Ho == H && Wo == W && C2 == 0 && !a2 &&
+      !rowbias && !resid && alpha == 1.f && out_dtype == PSO_BF16 && !accumulate && ldo == Cout && Cout <= 3 &&
+      pso_conv3x3_smallc_run(B, H, W, C1, Cout, src1, weight, bias, out, (hipStream_t)stream) == PSO_OK)
+    return PSO_OK;
   GemmArgs g{};
   const int Ct = C1 + C2;
   g.a1 = (const bf16_t*)src1; g.lda1 = 0; g.K1 = ks * ks * Ct;

@@ -97,6 +97,25 @@ def test_conv_normal(cuda, B, C1, C2, H, Cout, ks, stride):
     assert _rel(_nchw(out), ref) < 1e-5
 
 
+@pytest.mark.parametrize("B,C,H,W,Cout,bias", [(2, 128, 32, 48, 3, True), (1, 64, 16, 16, 3, False),
+                                                (3, 192, 48, 32, 2, True), (1, 128, 32, 32, 1, True),
+                                                (1, 128, 20, 20, 3, True)])
+def test_conv_small_cout_direct(cuda, B, C, H, W, Cout, bias):
+    """Cout <= 3 3x3 convolutions (the VAE decoder's conv_out to RGB) take the direct kernel (conv_small.hip) where
+    H, W are multiples of 16 -- the 20 x 20 case falls back to the implicit GEMM -- against an fp32 reference: bf16
+    output rounding is the only error (<= 4e-3 rel), image borders (zero padding) included."""
+    from pairwise_sample_optimization_amd import kernels as K_
+    x = torch.randn(B, C, H, W, device=cuda).bfloat16()
+    w = (torch.randn(Cout, C, 3, 3, device=cuda) / (3 * C ** 0.5)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16() if bias else None
+    ref = F.conv2d(x.float(), w.float(), b.float() if bias else None, padding=1)
+    out = K_.conv2d(_nhwc(x), _nhwc(w), bias=b)
+    direct = H % 16 == 0 and W % 16 == 0
+    assert K_.lib().pso_last_kernel().decode().startswith("conv3x3_smallc") == direct
+    assert _rel(_nchw(out), ref) < 4e-3
+    assert (_nchw(out).float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("C1,C2,Cout", [(1280, 0, 1280), (1280, 640, 640)])
 @pytest.mark.knobs
 def test_conv_splitk_workspace(cuda, C1, C2, Cout):
