@@ -17,7 +17,8 @@ def main():
                 name = r["Kernel_Name"].replace("void ", "").split("(")[0]
                 if pat not in name:
                     continue
-                grid = int(r.get("Grid_Size", 0) or 0)
+                grid = int(r.get("Grid_Size", 0) or 0) or (int(r.get("Grid_Size_X", 0) or 0) * int(r.get("Grid_Size_Y", 1) or 1) *
+                                                       int(r.get("Grid_Size_Z", 1) or 1))
                 agg[(name, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for (name, grid), v in sorted(agg.items()):
         v.sort()
