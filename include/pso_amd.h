@@ -308,7 +308,9 @@ int pso_layer_norm_bwd(int M, int C, const void* x, long ldx, const void* dy, lo
  * Replaces: F.scaled_dot_product_attention in diffusers AttnProcessor2_0 (attn1 self / attn2 cross attention of the
  *           140 SDXL BasicTransformerBlocks) and its autograd backward.
  * bwd: ws of pso_attention_bwd_ws_bytes(); for Sk <= 256 (cross-attention) dk/dv must be dense [B*Sk][.] with row
- *      stride lddk/lddv and batch stride Sk*ld.
+ *      stride lddk/lddv and batch stride Sk*ld.  Sk <= 96 (the 77 text tokens) runs ONE pass over the query tiles
+ *      for dQ, dK and dV (attn_bwd_x_kernel, query splits reduced in order: deterministic); longer key sequences run
+ *      the dQ and the dK/dV kernels.
  * ---------------------------------------------------------------------------------------------------------------- */
 int pso_attention_fwd(int B, int H, int Sq, int Sk, const void* q, long ldq, long sq_b, const void* k, long ldk,
                       long sk_b, const void* v, long ldv, long sv_b, float scale, void* o, long ldo, long so_b,

@@ -25,7 +25,9 @@ void pso_gemm8p_skip_epilogue(int on);
 void pso_gemm_tn_set_split(int ks);
 /* Attention: ones digit = forward form (0 auto, 1 lane-local growth test, 2 / 4 force 32 / 64 rows per wave, 5-9 the
  * first-round loop), tens digit = backward form (0 default, 1 / 3 older forms, 4 64 keys per wave, 5 / 6 deeper
- * rings, 8 / 9 the 8-wave ping-pong dK/dV), 100s = VALU row sums, 1000s = segment clock trace of the ping-pong form. */
+ * rings, 7 the dQ + dK/dV launches for short key sequences too (instead of the one-pass attn_bwd_x_kernel), 8 / 9 the
+ * 8-wave ping-pong dK/dV), 100s = VALU row sums, 1000s = segment clock trace of the ping-pong form, 10000 * qs = the
+ * query splits of attn_bwd_x_kernel (0 automatic). */
 void pso_attention_set_variant(int v);
 /* Segment-start clocks of the last traced ping-pong dK/dV launch (2 x 520 unsigned 64-bit, group-major). */
 int pso_attn_pp_trace(unsigned long long* out);

@@ -842,6 +842,280 @@ __global__ __launch_bounds__(ATT_THREADS, KJ == 2 ? 2 : 1) void attn_bwd_dkv_ker
 }
 
 // ================================================================================================================
+// backward for short key sequences (cross-attention over the 77 text tokens, Sk <= XK_KP = 96): ONE pass over the
+// query tiles makes dQ, dK and dV.  attn_bwd_dkv_kernel's structure (4 waves x 32 keys on the MFMA lane axis, so all
+// keys of the (batch, head) sit in one workgroup; query tiles of 64 through a 2-stage LDS-DMA ring, query splits
+// reduced by reduce_splits_kernel), plus:
+//   * the output O as a third ring image: -delta = -rowsum(dO * O) of the tile's 64 queries is formed in the kernel
+//     (the dQ kernel's lane pattern and summation order), so neither a dQ launch nor a delta pre-pass runs;
+//   * dQ of the tile: dS is written to LDS transposed ([key][query], 4 consecutive queries per lane: ds_write_b64), and
+//     wave w forms dQ^T for queries 16w .. 16w+15 against an LDS image of K (staged once; rows past Sk zero):
+//     dQ^T[d][q] = sum_k K^T[d][k] dS^T[k][q], both fragments by transposed reads, 4 consecutive d per lane on store.
+// Versus the dQ + dK/dV + reduce launches it skips the dQ kernel's second S / dP / exp sweep over the same queries.
+// ================================================================================================================
+#define XK_KP 96  // key rows of the K / dS^T images (multiple of 32: whole 32-deep MFMA steps)
+__global__ __launch_bounds__(ATT_THREADS, 2) void attn_bwd_x_kernel(AttnArgs a) {
+  constexpr int KJ = 2, STG = 2;
+  constexpr int IMG = ATT_KT * ATT_D;  // one 64 x 64 image
+  constexpr int NIMG = 3;              // Q^T, dO^T, O^T (swz_tr layout: row and transposed reads)
+  constexpr int PIECES = 2 * NIMG;     // 16-B glds per wave per tile (+1 LSE dword piece on wave 0)
+  __shared__ __attribute__((aligned(16))) bf16_t sRing[STG][NIMG][IMG];
+  __shared__ __attribute__((aligned(16))) float sLD[STG][2][64];  // LSE (natural, by DMA), -delta (formed here)
+  __shared__ __attribute__((aligned(16))) bf16_t sK[XK_KP * ATT_D];    // K rows 0 .. XK_KP-1 (swz_tr), zero past Sk
+  __shared__ __attribute__((aligned(16))) bf16_t sDS[XK_KP * ATT_D];   // dS^T [key][query of the tile] (swz_tr)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / a.q_split, split = bid - bh * a.q_split;
+  const int h = bh % a.H, b = bh / a.H;
+  const int k0 = wave * (16 * KJ);
+
+  const bf16_t* Q = a.q + b * a.sq_b + h * ATT_D;
+  const bf16_t* K = a.k + b * a.sk_b + h * ATT_D;
+  const bf16_t* V = a.v + b * a.sv_b + h * ATT_D;
+  const bf16_t* DO = a.dO + b * a.sdo_b + h * ATT_D;
+  const bf16_t* Y = a.o + b * a.so_b + h * ATT_D;
+  const float* LSE = a.lse + ((long)b * a.H + h) * a.Sq;
+  const float c2 = a.scale_log2;
+  const float ln2inv = 1.4426950408889634f;
+
+  const int nqt = (a.Sq + ATT_KT - 1) / ATT_KT;
+  const int per = (nqt + a.q_split - 1) / a.q_split;
+  const int qa = split * per, qb = min(nqt, qa + per);
+  const int n = qb > qa ? qb - qa : 0;
+
+  const int prow = lane >> 3, pch = lane & 7;
+  const int lcT = pch ^ (2 * ((prow >> 1) & 3));
+  const __amdgpu_buffer_rsrc_t rQ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)(((long)(a.Sq - 1) * a.ldq + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)DO, (short)0, (int)(((long)(a.Sq - 1) * a.lddo + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rY =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, (int)(((long)(a.Sq - 1) * a.ldo + ATT_D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)LSE, (short)0, a.Sq * 4, 0x00020000);
+  unsigned qto[2], dto[2], yto[2];
+#pragma unroll
+  for (int pw = 0; pw < 2; ++pw) {
+    const int row = (wave * 2 + pw) * 8 + prow;
+    qto[pw] = (unsigned)(row * (int)a.ldq + lcT * 8) * 2u;
+    dto[pw] = (unsigned)(row * (int)a.lddo + lcT * 8) * 2u;
+    yto[pw] = (unsigned)(row * (int)a.ldo + lcT * 8) * 2u;
+  }
+  const int qstep = ATT_KT * (int)a.ldq * 2, dstep = ATT_KT * (int)a.lddo * 2, ystep = ATT_KT * (int)a.ldo * 2;
+  auto issue = [&](int qt, int buf) {
+    if (wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rL, (att_lds_void*)(&sLD[buf][0][0]), 4, lane * 4, qt * ATT_KT * 4, 0, 0);
+#pragma unroll
+    for (int pw = 0; pw < 2; ++pw) {
+      const int piece = wave * 2 + pw;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rQ, (att_lds_void*)(sRing[buf][0] + piece * 8 * ATT_D), 16, qto[pw],
+                                               qt * qstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rD, (att_lds_void*)(sRing[buf][1] + piece * 8 * ATT_D), 16, dto[pw],
+                                               qt * dstep, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rY, (att_lds_void*)(sRing[buf][2] + piece * 8 * ATT_D), 16, yto[pw],
+                                               qt * ystep, 0, 0);
+    }
+  };
+
+  // K / V fragments of this wave's 32 keys (B operands; keys past Sk clamped: computed, never stored, their dS is
+  // dropped before it reaches dQ); the K image for dQ (rows past Sk zero)
+  bf16x8 kf[KJ][2], vf[KJ][2];
+#pragma unroll
+  for (int kj = 0; kj < KJ; ++kj) {
+    const int kr = min(k0 + kj * 16 + c, a.Sk - 1);
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      kf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(K + (long)kr * a.ldk + ds * 32 + 8 * g));
+      vf[kj][ds] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(V + (long)kr * a.ldv + ds * 32 + 8 * g));
+    }
+  }
+  for (int e = tid; e < XK_KP * 8; e += ATT_THREADS) {
+    const int row = e >> 3, ch = e & 7;
+    const uint4 v = row < a.Sk ? *reinterpret_cast<const uint4*>(K + (long)row * a.ldk + ch * 8) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(sK + swz_tr(row, ch)) = v;
+  }
+  unsigned troff[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int li = lane & 15;
+    const int col = dt * 16 + 4 * (li & 3);
+    troff[dt] = 2u * (unsigned)(swz_tr(4 * g + (li >> 2), col >> 3) + (col & 7));
+  }
+  f32x4 dk[KJ][4], dv[KJ][4];
+#pragma unroll
+  for (int kj = 0; kj < KJ; ++kj)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[kj][dt] = dv[kj][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float sc = a.scale_log2 * 0.69314718055994531f;  // the softmax scale (dQ and dK carry it)
+  const int nks = (min(a.Sk, XK_KP) + 31) >> 5;           // 32-key steps of dQ that hold a key
+
+  // -delta of a landed tile's 64 queries into sLD[buf][1]: wave w, lane (g, c) -> query 16w + c, d chunks 4 ds + g
+  // (the dQ kernel's lanes and summation order)
+  auto form_delta = [&](int buf) {
+    const int qr = wave * 16 + c;
+    float part = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) {
+      const uint4 w = *reinterpret_cast<const uint4*>(sRing[buf][1] + swz_tr(qr, ds * 4 + g));
+      const uint4 u = *reinterpret_cast<const uint4*>(sRing[buf][2] + swz_tr(qr, ds * 4 + g));
+      const uint32_t ow[4] = {u.x, u.y, u.z, u.w}, dw[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        part += bf2f(ow[j] & 0xffff) * bf2f(dw[j] & 0xffff) + bf2f(ow[j] >> 16) * bf2f(dw[j] >> 16);
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    if (g == 0) sLD[buf][1][qr] = -part;
+  };
+  // Per tile two barriers: (A) at the top -- tile i landed, its -delta formed (during tile i - 1's dQ phase), every
+  // read of the previous tile's sDS done; (B) after the dS^T writes -- tile i + 1 landed too, so its -delta is formed
+  // beside tile i's dQ MFMAs.
+  if (n > 0) {
+    issue(qa, 0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    form_delta(0);
+  }
+  for (int i = 0; i < n; ++i) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (A): no vmcnt -- the last dQ stores stay in flight
+    if (i + 1 < n) issue(qa + i + 1, (i + 1) % STG);
+    const int buf = i % STG;
+    const bf16_t* sQt = sRing[buf][0];
+    const bf16_t* sOt = sRing[buf][1];
+    float4 lpf[4], dpf[4];
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      lpf[qs] = *reinterpret_cast<const float4*>(&sLD[buf][0][qs * 16 + 4 * g]);
+      dpf[qs] = *reinterpret_cast<const float4*>(&sLD[buf][1][qs * 16 + 4 * g]);
+    }
+#pragma unroll
+    for (int qk = 0; qk < 2; ++qk) {
+      f32x4 p[2][KJ], dsv[2][KJ];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const int qs = 2 * qk + qh;
+        bf16x8 qa_[2], oa_[2];
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          const int ro = swz_tr(qs * 16 + c, d2 * 4 + g);
+          qa_[d2] = *reinterpret_cast<const bf16x8*>(sQt + ro);
+          oa_[d2] = *reinterpret_cast<const bf16x8*>(sOt + ro);
+        }
+        // rows past Sq read as zeros (Q, dO, O and the LSE resources end at row Sq - 1): S = 0, p = 1, dP = 0,
+        // delta = 0, dS = 0 -- they add nothing to dK / dV and their dQ rows are not stored
+        const float lq[4] = {lpf[qs].x * ln2inv, lpf[qs].y * ln2inv, lpf[qs].z * ln2inv, lpf[qs].w * ln2inv};
+        const f32x4 ndel = {dpf[qs].x, dpf[qs].y, dpf[qs].z, dpf[qs].w};
+#pragma unroll
+        for (int kj = 0; kj < KJ; ++kj) {
+          f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, pacc = ndel;
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[0], kf[kj][0], sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa_[1], kf[kj][1], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[0], vf[kj][0], pacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa_[1], vf[kj][1], pacc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = fast_exp2(fmaf(sacc[r], c2, -lq[r]));
+            p[qh][kj][r] = pr;
+            dsv[qh][kj][r] = pr * pacc[r];
+          }
+          // dS^T for dQ: key row k, queries qs*16 + 4g .. +3 (8 B); keys past Sk (clamped duplicates) are zero
+          const int kr = k0 + kj * 16 + c;
+          if (kr < XK_KP) {
+            const bool live = kr < a.Sk;
+            const uint2 wv = live ? make_uint2(pack2bf(dsv[qh][kj][0], dsv[qh][kj][1]), pack2bf(dsv[qh][kj][2], dsv[qh][kj][3]))
+                                  : make_uint2(0u, 0u);
+            const int col = qs * 16 + 4 * g;
+            *reinterpret_cast<uint2*>(sDS + swz_tr(kr, col >> 3) + (col & 7)) = wv;
+          }
+        }
+      }
+      bf16x8 of[4], qf[4];
+      {
+        s16x4 otr[8], qtr[8];
+        const unsigned qtb = (unsigned)(uintptr_t)(const att_lds_void*)sQt;
+        const unsigned otb = (unsigned)(uintptr_t)(const att_lds_void*)sOt;
+        auto trd = [&](auto QK_) {
+          constexpr int o = decltype(QK_)::value * 4096;  // query rows 32 qk ..
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            qtr[2 * dt] = tr_read_imm<o>(qtb + troff[dt]);
+            qtr[2 * dt + 1] = tr_read_imm<o + 2048>(qtb + troff[dt]);
+            otr[2 * dt] = tr_read_imm<o>(otb + troff[dt]);
+            otr[2 * dt + 1] = tr_read_imm<o + 2048>(otb + troff[dt]);
+          }
+        };
+        if (qk == 0) trd(ic<0>{});
+        else trd(ic<1>{});
+        lds_wait8(otr);
+        lds_wait8(qtr);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          of[dt] = cat_frag(otr[2 * dt], otr[2 * dt + 1]);
+          qf[dt] = cat_frag(qtr[2 * dt], qtr[2 * dt + 1]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+        for (int kj = 0; kj < KJ; ++kj) {
+          dv[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of[dt], pack_p(p[0][kj], p[1][kj]), dv[kj][dt], 0, 0, 0);
+          dk[kj][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[dt], pack_p(dsv[0][kj], dsv[1][kj]), dk[kj][dt], 0, 0, 0);
+        }
+      }
+    }
+    // dQ^T of queries 16 wave .. +15 of the tile: A = K^T (16 d x 32 keys), B = dS^T (32 keys x 16 queries), both by
+    // transposed reads in natural key order (rows 8g .. 8g+7 of each 32-key step)
+    att_wait_barrier<PIECES>(0);  // (B): every wave's dS^T written, tile i + 1 landed
+    if (i + 1 < n) form_delta((i + 1) % STG);
+    {
+      f32x4 dq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int st = 0; st < nks; ++st) {
+        const int r0 = st * 32 + 8 * g;
+        const bf16x8 bfr = cat_frag(tr_read(sDS, r0, wave * 16, lane), tr_read(sDS, r0 + 4, wave * 16, lane));
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x8 kfr = cat_frag(tr_read(sK, r0, dt * 16, lane), tr_read(sK, r0 + 4, dt * 16, lane));
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfr, bfr, dq[dt], 0, 0, 0);
+        }
+      }
+      const int qr = (qa + i) * ATT_KT + wave * 16 + c;
+      if (qr < a.Sq) {
+        bf16_t* dQ = a.dq + b * a.sdq_b + (long)qr * a.lddq + h * ATT_D;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *reinterpret_cast<uint2*>(dQ + dt * 16 + 4 * g) =
+              make_uint2(pack2bf(dq[dt][0] * sc, dq[dt][1] * sc), pack2bf(dq[dt][2] * sc, dq[dt][3] * sc));
+      }
+    }
+  }
+  // dK / dV epilogue (lane holds d?[k = k0 + kj*16 + c][d = dt*16 + 4g + r]), as attn_bwd_dkv_kernel
+#pragma unroll
+  for (int kj = 0; kj < KJ; ++kj) {
+    const int kr = k0 + kj * 16 + c;
+    if (kr >= a.Sk) continue;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = h * ATT_D + dt * 16 + 4 * g;
+      if (a.q_split > 1) {
+        const long slice = (long)split * (a.nbatch * (long)a.Sk) * (a.H * ATT_D);
+        float* pk = a.dk_acc + slice + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
+        float* pv = a.dv_acc + slice + ((long)b * a.Sk + kr) * (a.H * ATT_D) + d;
+        *reinterpret_cast<float4*>(pk) = make_float4(dk[kj][dt][0] * sc, dk[kj][dt][1] * sc, dk[kj][dt][2] * sc,
+                                                     dk[kj][dt][3] * sc);
+        *reinterpret_cast<float4*>(pv) = make_float4(dv[kj][dt][0], dv[kj][dt][1], dv[kj][dt][2], dv[kj][dt][3]);
+      } else {
+        *reinterpret_cast<uint2*>(a.dk + b * a.sdk_b + (long)kr * a.lddk + d) =
+            make_uint2(pack2bf(dk[kj][dt][0] * sc, dk[kj][dt][1] * sc), pack2bf(dk[kj][dt][2] * sc, dk[kj][dt][3] * sc));
+        *reinterpret_cast<uint2*>(a.dv + b * a.sdv_b + (long)kr * a.lddv + d) =
+            make_uint2(pack2bf(dv[kj][dt][0], dv[kj][dt][1]), pack2bf(dv[kj][dt][2], dv[kj][dt][3]));
+      }
+    }
+  }
+}
+
+// ================================================================================================================
 // backward dK/dV, ping-pong form: one workgroup = 8 waves = 256 keys of one (b, h), 32 per wave as in the form above
 // (same arithmetic, same accumulation order: bit-identical dK / dV).  Waves w and w + 4 share a SIMD; the two groups
 // (waves 0-3 / 4-7) share one Q / dO query-tile ring and run one segment apart, every query tile being two segments
@@ -1362,25 +1636,33 @@ __global__ void reduce_splits_kernel(long rows, int cols, int nsplit, const floa
   }
 }
 
-// Query splits of the dK/dV sweep when there are few key blocks (cross-attention over the 77 text tokens): enough
-// workgroups for ~2 per CU; each split writes its own fp32 partial slice (no atomics).
-static int cross_qsplit(int B, int H, int Sq, int Sk) {
-  if (Sk > 256) return 1;
-  const int nqt = cdiv(Sq, ATT_KT);
-  int qs = cdiv(512, (long)cdiv(Sk, 128) * H * B);
-  if (qs > nqt) qs = nqt;
-  return qs < 1 ? 1 : qs;
-}
-
 // benchmark knobs (tools build only; compile-time zeros in the product library, whose dispatch is the default forms)
 #ifdef PSO_BENCH_KNOBS
 static int g_attn_fwd_variant = 0;
 static bool g_attn_vsum = false;
 static int g_attn_bwd_variant = 0;  // benchmark knob (the tens digit of pso_attention_set_variant): see pso_attention_bwd
 static bool g_attn_pp_trace = false;  // the ping-pong dK/dV form records segment clocks (diagnostic)
+static int g_attn_xqs = 0;  // query splits of the short-KV backward (0 = automatic)
 #else
-static constexpr int g_attn_fwd_variant = 0, g_attn_bwd_variant = 0;
+static constexpr int g_attn_fwd_variant = 0, g_attn_bwd_variant = 0, g_attn_xqs = 0;
 #endif
+
+// Query splits of the dK/dV sweep when there are few key blocks (cross-attention over the 77 text tokens): enough
+// workgroups for ~2 per CU; each split writes its own fp32 partial slice (no atomics).
+static int cross_qsplit(int B, int H, int Sq, int Sk) {
+  if (Sk > 256) return 1;
+  if (Sk <= XK_KP && g_attn_bwd_variant != 7) {  // attn_bwd_x_kernel: at most one round of its 512 co-resident slots
+    int qs = g_attn_xqs > 0 ? g_attn_xqs : 512 / (H * B);
+    const int nqt = cdiv(Sq, ATT_KT);
+    if (qs > nqt) qs = nqt;
+    return qs < 1 ? 1 : qs;
+  }
+  const int nqt = cdiv(Sq, ATT_KT);
+  int qs = cdiv(512, (long)cdiv(Sk, 128) * H * B);
+  if (qs > nqt) qs = nqt;
+  return qs < 1 ? 1 : qs;
+}
+
 
 static bool a16(const void* p, long ld) { return (((uintptr_t)p) & 15) == 0 && (ld % 8) == 0; }
 
@@ -1397,6 +1679,7 @@ void pso_attention_set_variant(int v) {
   g_attn_bwd_variant = (v / 10) % 10;
   g_attn_vsum = (v / 100) % 10 == 1;  // 100+: row sums on the VALU (A/B knob)
   g_attn_pp_trace = (v / 1000) % 10 == 1;
+  g_attn_xqs = (v / 10000) % 100;  // 10000 * qs: the short-KV backward's query splits
 }
 #endif
 
@@ -1491,6 +1774,10 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
   // 3-5 % faster on the self-attention shapes (L1 1.113 vs 1.157 ms, L2 0.168 vs 0.177 ms, medians of 4 alternated
   // runs, profiles/r05_attn_bwd_ab.log); 5 / 6 = ONE with rings of 3 / 4 (no faster)
   const dim3 gq(cdiv(Sq, 128), H, B);
+  const bool xpath = Sk <= XK_KP && g_attn_bwd_variant != 7;  // 7: the dQ + dK/dV launches (A/B knob)
+  if (xpath) {  // short key sequences (cross-attention): dQ, dK and dV in one pass over the query tiles
+    attn_bwd_x_kernel<<<dim3(qsplit * H * B), ATT_THREADS, 0, st>>>(a);
+  } else {
 #ifdef PSO_BENCH_KNOBS
   const int bv = g_attn_bwd_variant;
   if (bv == 3 || bv == 1) attn_bwd_dq_kernel<3, false><<<gq, ATT_THREADS, 0, st>>>(a);
@@ -1556,6 +1843,7 @@ int pso_attention_bwd(int B, int H, int Sq, int Sk, const void* q, long ldq, lon
     attn_bwd_dkv_kernel<2, 2, true, true><<<dim3(nkb * qsplit * H * B), ATT_THREADS, shm, st>>>(a, nkb);
   }
 #endif
+  }
   if (qsplit > 1) {
     // dk/dv outputs are [B][Sk] rows of H*64 with row stride lddk (batch stride must be Sk*lddk)
     const long rows = (long)B * Sk;

@@ -103,7 +103,8 @@ def test_attention_fwd_bit_deterministic_eager_and_graph(cuda, shape, spike):
 def test_attention_bwd_forms_bit_identical(cuda, shape, spike):
     """The dK/dV / dQ forms give the same bits: the default one-image LDS ring (Q / dO staged once in the transposed-read
     layout), the two-image ring (bwd variant 3) and the 8-wave ping-pong dK/dV (variant 8, and 9 at raised priority;
-    self-attention only -- cross-attention keeps the query-split form), each reproducible run to run, on
+    self-attention only -- the 77-key cross-attention runs the one-pass attn_bwd_x_kernel under every variant but 7,
+    whose dQ + dK/dV launches are checked against the same fp32 reference), each reproducible run to run, on
     ragged (1000-token) and spiked inputs; and the default matches an fp32 autograd reference."""
     from pairwise_sample_optimization_amd import kernels as K
     B, H, Sq, Sk = shape
@@ -113,7 +114,7 @@ def test_attention_bwd_forms_bit_identical(cuda, shape, spike):
     do = torch.randn(B, Sq, H * 64, device=cuda, generator=g).bfloat16()
     grads = {}
     # 30: two-image ring, 50 / 60: one-image rings of 3 / 4 stages, 80 / 90: 8-wave ping-pong dK/dV (tools build)
-    for variant in _variants(0, 30, 50, 60, 80, 90):
+    for variant in _variants(0, 30, 50, 60, 80, 90, *([70] if Sk <= 96 else [])):
         def go():
             a = [x.clone() for x in K.attention_bwd(q, k, v, o, lse, do, H)]
             b = K.attention_bwd(q, k, v, o, lse, do, H)
@@ -122,7 +123,7 @@ def test_attention_bwd_forms_bit_identical(cuda, shape, spike):
         for x, y in zip(a, b):
             assert torch.equal(x, y), f"bwd variant {variant}: not reproducible"
         grads[variant] = a
-    for variant in [v for v in grads if v]:
+    for variant in [v for v in grads if v and v != 70]:
         for name, x, y in zip(("dq", "dk", "dv"), grads[variant], grads[0]):
             assert torch.equal(x, y), f"bwd variant {variant}: {name} differs from the default form"
     # fp32 reference on two heads
@@ -130,9 +131,12 @@ def test_attention_bwd_forms_bit_identical(cuda, shape, spike):
                        for t in (q, k, v, do))
     ref = torch.softmax(qf @ kf.transpose(-1, -2) / 8.0, -1) @ vf
     ref.backward(dof)
-    for name, mine, r in zip(("dq", "dk", "dv"), grads[0], (qf.grad, kf.grad, vf.grad)):
-        m = mine.float().view(B, -1, H, 64)[:, :, :2].transpose(1, 2)
-        assert ((m - r).norm() / r.norm()).item() < 2e-2, name
+    for variant, gv in grads.items():
+        if variant not in (0, 70):
+            continue
+        for name, mine, r in zip(("dq", "dk", "dv"), gv, (qf.grad, kf.grad, vf.grad)):
+            m = mine.float().view(B, -1, H, 64)[:, :, :2].transpose(1, 2)
+            assert ((m - r).norm() / r.norm()).item() < 2e-2, (variant, name)
 
 
 @pytest.mark.knob_variants

@@ -90,6 +90,36 @@ def test_attention_fwd_bwd(cuda, B, H, Sq, Sk):
     assert _rel(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,Sq,Sk", [(2, 5, 300, 77), (4, 10, 4096, 77), (2, 20, 1024, 77), (1, 3, 64, 96),
+                                        (3, 2, 190, 33), (1, 1, 1, 5), (16, 20, 1024, 77)])
+def test_attention_bwd_short_kv_fused(cuda, B, H, Sq, Sk):
+    """The short-key backward (Sk <= 96: the cross-attention over the 77 text tokens) makes dQ, dK and dV in one pass
+    over the query tiles (attn_bwd_x_kernel; -delta formed in the kernel, dQ through an LDS dS^T tile), with and
+    without query splits, ragged query tiles, Sk not a multiple of 16 or 32: against fp32 autograd, and bit-reproducible
+    run to run."""
+    from pairwise_sample_optimization_amd import kernels as K
+    C = H * 64
+    g = torch.Generator(device="cuda").manual_seed(11 * Sq + Sk)
+    q = torch.randn(B, Sq, C, device=cuda, generator=g).bfloat16()
+    k = torch.randn(B, Sk, C, device=cuda, generator=g).bfloat16()
+    v = torch.randn(B, Sk, C, device=cuda, generator=g).bfloat16()
+    do = torch.randn(B, Sq, C, device=cuda, generator=g).bfloat16()
+    o, lse = K.attention_fwd(q, k, v, H)
+    a = [x.clone() for x in K.attention_bwd(q, k, v, o, lse, do, H)]
+    b = K.attention_bwd(q, k, v, o, lse, do, H)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    hs = min(H, 4)  # fp32 reference on the first heads
+    f = lambda t: t.float().view(B, -1, H, 64)[:, :, :hs].transpose(1, 2).detach().requires_grad_(True)
+    qf, kf, vf = f(q), f(k), f(v)
+    ref = torch.softmax(qf @ kf.transpose(-1, -2) / 8.0, -1) @ vf
+    ref.backward(do.float().view(B, -1, H, 64)[:, :, :hs].transpose(1, 2))
+    for name, mine, r in zip(("dq", "dk", "dv"), a, (qf.grad, kf.grad, vf.grad)):
+        m = mine.float().view(B, -1, H, 64)[:, :, :hs].transpose(1, 2)
+        assert ((m - r).norm() / r.norm()).item() < 2e-2, name
+        assert torch.isfinite(mine).all(), name
+
+
 @pytest.mark.parametrize("B,H,Sq,Sk", [(2, 5, 300, 77), (1, 2, 100, 100), (1, 4, 130, 1000)])
 def test_attention_partial_tiles_poisoned_tail(cuda, B, H, Sq, Sk):
     """Partial last key / query tiles with NaN in the memory right past the last row of Q, K, V and dO: the staging
