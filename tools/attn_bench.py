@@ -32,6 +32,8 @@ def main():
               ("L2 cross", Bi, 20, 1024, 77)]
     if os.environ.get("ATTN_CROSS_ONLY"):
         shapes = [x for x in shapes if x[4] <= 128]
+    if os.environ.get("ATTN_SHAPE"):  # one level only, e.g. "L2 cross"
+        shapes = [x for x in shapes if x[0] == os.environ["ATTN_SHAPE"]]
     ref = {}
     for v in [int(x) for x in os.environ.get("ATTN_VARIANTS", "0").split(",")]:
         K.lib().pso_attention_set_variant(v)
