@@ -5,7 +5,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-xattn}
 mkdir -p gpurun_out && rm -rf gpurun_out/${T}_trace
-export ATTN_CROSS_ONLY=1
+[ -z "${ATTN_SHAPE:-}" ] && export ATTN_CROSS_ONLY=1
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_trace -o run -- \
     python3 tools/attn_bench.py > gpurun_out/${T}_bench.txt 2>&1 || { tail -20 gpurun_out/${T}_bench.txt; exit 1; }
 python3 tools/trace_by_grid.py gpurun_out/${T}_trace attn > gpurun_out/${T}_kernels.txt && cat gpurun_out/${T}_kernels.txt
